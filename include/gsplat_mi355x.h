@@ -1,0 +1,229 @@
+/*
+ * gsplat_mi355x.h -- C ABI of the MI355X (gfx950) Gaussian-splatting rasterizer.
+ *
+ * Drop-in boundary for GaussianRenderer.render() of
+ * Loveof1ife7/mini-3d-gaussian-splatting (src/core/renderer.py:31-367) and the
+ * autograd backward the reference gets from torch.  Every stage of the
+ * reference's render pipeline maps to one entry point below; each entry
+ * point cites the reference function it replaces.
+ *
+ * Conventions
+ *  - Plain C: raw device pointers, sizes, POD structs.  No torch types.
+ *  - Stream ordered: every function enqueues work on `stream` (a hipStream_t
+ *    passed as void*) and returns without synchronising.
+ *  - Caller owns all memory.  The library never allocates; scratch comes from
+ *    caller-provided workspaces whose sizes the *_workspace_bytes() queries
+ *    return.
+ *  - Errors: every entry point returns a gs_status; gs_last_error() returns a
+ *    thread-local message for the last non-OK status on the calling thread.
+ *    Nothing aborts or exits.
+ *  - Re-entrant: no mutable globals; safe from several host threads on
+ *    different streams.
+ *  - fp32 throughout (the reference computes in fp32).
+ */
+#ifndef GSPLAT_MI355X_H
+#define GSPLAT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+#define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
+#define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
+#define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian) gradient slot */
+#define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2..3] reserved */
+
+typedef enum gs_status {
+  GS_OK = 0,
+  GS_ERR_INVALID_ARG = 1,
+  GS_ERR_LAUNCH = 2,
+  GS_ERR_UNSUPPORTED = 3
+} gs_status;
+
+typedef void *gs_stream_t; /* hipStream_t */
+
+/* Camera + settings as the reference renderer reads them.
+ * fx,fy,cx,cy come from camera._width/_height/_FoVx/_FoVy exactly as
+ * renderer.py:140-147 computes them (python double, rounded to fp32);
+ * view is rows 0..2 of camera.world_view_transform() (renderer.py:150-152,
+ * untransposed, column-vector convention). */
+typedef struct gs_camera {
+  int32_t image_width;   /* RenderSettings.image_width  (renderer.py:60) */
+  int32_t image_height;  /* RenderSettings.image_height */
+  float fx, fy, cx, cy;
+  float view[12];        /* row-major 3x4 [R | t] */
+  float radius_min;      /* GaussianRenderer(radius_min=0.01) */
+  float radius_max;      /* GaussianRenderer(radius_max=50.0) */
+  float bg[3];           /* RenderSettings.bg_color */
+  int32_t tile_size;     /* must be GS_TILE */
+} gs_camera;
+
+/* Gaussian inputs (the duck-typed GaussianModel accessors).
+ * Covariance: either cov3d ([n,9] row-major, = get_covariance) or the raw
+ * parameters scaling ([n,3] log-sigma) + rotation ([n,4] q=[w,x,y,z], not
+ * necessarily normalised), from which the kernel builds
+ * R(normalize(q)) diag(exp(s)^2) R^T as gaussian_model.py:200-207 does. */
+typedef struct gs_gaussians {
+  int32_t n;
+  const float *xyz;          /* [n, xyz_stride] get_xyz */
+  int64_t xyz_stride;        /* floats between rows (3 if contiguous) */
+  const float *cov3d;        /* [n,9] or NULL */
+  const float *scaling;      /* [n,3] raw, used when cov3d == NULL */
+  const float *rotation;     /* [n,4] raw, used when cov3d == NULL */
+  const float *color_logits; /* [n, color_stride] get_features[:,0,:] (pre-sigmoid, renderer.py:88-92) */
+  int64_t color_stride;
+  const float *opacity;      /* [n, opacity_stride] get_opacity.squeeze(1) as given (renderer.py:94) */
+  int64_t opacity_stride;
+} gs_gaussians;
+
+/* ---- Stage 1: _project_gaussians_3d_to_2d + _frustum_culling ----------
+ * Replaces renderer.py:117-200 and :201-220.  One thread per Gaussian.
+ * Writes the render() outputs means2d (viewspace_points), conics, radii and
+ * visibility_filter, plus the splat record, tile rectangle and depth sort
+ * key used by the later stages.  counters[0] receives M (visible count);
+ * the callee zeroes counters first. */
+typedef struct gs_project_args {
+  gs_camera cam;
+  gs_gaussians g;
+  float *means2d;       /* [n,2] */
+  float *conics;        /* [n,4] = [n,2,2] */
+  float *radii;         /* [n]   */
+  uint8_t *vis;         /* [n]   torch.bool storage */
+  float *records;       /* [n, GS_RECORD_FLOATS] */
+  uint32_t *rects;      /* [n,2] packed tile rectangle */
+  uint32_t *depth_keys; /* [n]   fp32 bits of Z if visible, else 0xFFFFFFFF */
+  uint32_t *counters;   /* [GS_NUM_COUNTERS] */
+} gs_project_args;
+gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream);
+
+/* ---- Stage 2 / 4: device LSD radix sort (u32 key, u32 value) -----------
+ * Replaces torch.argsort in _sort_gaussians_by_depth (renderer.py:231-237)
+ * and the per-tile list build (:277-298).  Stable.  Sorts bits
+ * [begin_bit, end_bit) of keys in ceil((end-begin)/8) passes, ping-ponging
+ * between (keys, vals) and (keys_alt, vals_alt); *result_in_alt tells the
+ * caller which pair holds the result (known on the host without a sync).
+ * vals_are_iota != 0: the first pass reads values 0..n-1 instead of vals
+ * (vals is still used as ping-pong storage). */
+size_t gs_radix_sort_workspace_bytes(int32_t n);
+gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt,
+                              uint32_t *vals_alt, int32_t n, int32_t begin_bit,
+                              int32_t end_bit, int32_t vals_are_iota, void *workspace,
+                              size_t workspace_bytes, int32_t *result_in_alt,
+                              gs_stream_t stream);
+
+/* ---- Stage 3: tile binning (renderer.py:263-298) ----------------------
+ * gs_bin_count: per-Gaussian tile-touch counts in depth order, reduced to
+ *   per-block partial sums and scanned; counters[1] receives T.
+ * gs_bin_emit : one (tile id, pair index) entry per touched tile, emitted in
+ *   depth order (so a stable sort by tile keeps depth order inside a tile);
+ *   pair_gauss[e] = Gaussian of entry e, pair_offset[g] = first entry of g. */
+size_t gs_bin_workspace_bytes(int32_t n);
+typedef struct gs_bin_args {
+  int32_t n;
+  int32_t tiles_x, tiles_y;
+  const uint32_t *sorted_ids; /* [n] depth-sorted Gaussian ids (visible first) */
+  const uint32_t *rects;      /* [n,2] from gs_project_forward */
+  uint32_t *counters;         /* [GS_NUM_COUNTERS] */
+  void *workspace;
+  size_t workspace_bytes;
+  /* emit outputs (ignored by gs_bin_count) */
+  uint32_t *tile_keys;   /* [T] */
+  uint32_t *pair_gauss;  /* [T] */
+  uint32_t *pair_offset; /* [n] indexed by Gaussian id */
+} gs_bin_args;
+gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream);
+gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream);
+
+/* Per-tile [start,end) ranges of the tile-sorted entries, and the Gaussian
+ * id of each sorted entry.  Replaces the tile_lists of renderer.py:266. */
+typedef struct gs_range_args {
+  int32_t num_pairs;           /* T */
+  int32_t num_tiles;
+  const uint32_t *sorted_keys; /* [T] tile ids, sorted */
+  const uint32_t *sorted_pairs;/* [T] entry index e, in tile-sorted order */
+  const uint32_t *pair_gauss;  /* [T] */
+  uint32_t *ranges;            /* [num_tiles,2] */
+  uint32_t *sorted_gauss;      /* [T] */
+} gs_range_args;
+gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream);
+
+/* ---- Stage 5: _tile_rasterization blend, forward -------------------------
+ * renderer.py:273-367: per pixel (integer coordinates) front-to-back alpha
+ * compositing of its tile's list, termination once A >= 0.995, background
+ * composite (bg counted twice, as the reference does), clamps, depth
+ * normalisation.  One 256-thread workgroup per 16x16 tile.  pix_state
+ * keeps what the backward needs: [H*W] float4 (acc_r, acc_g, acc_b, D) and
+ * [H*W] float2 (A, bits of n_eval). */
+typedef struct gs_blend_fwd_args {
+  gs_camera cam;
+  int32_t tiles_x, tiles_y;
+  const uint32_t *ranges;       /* [num_tiles,2] */
+  const uint32_t *sorted_gauss; /* [T] */
+  const float *records;         /* [n, GS_RECORD_FLOATS] */
+  float *image;                 /* [3,H,W] */
+  float *alpha;                 /* [H,W]   */
+  float *depth;                 /* [H,W]   */
+  float *pix_acc;               /* [H*W,4] */
+  float *pix_state;             /* [H*W,2] */
+} gs_blend_fwd_args;
+gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
+
+/* ---- Backward of the blend -------------------------------------------
+ * Re-walks each pixel's list front-to-back (bit-identical replay of the
+ * forward's decisions) and writes one gradient slot per (tile, Gaussian)
+ * entry: pair_grads[e] = {dmu_x, dmu_y, dQ00, dQ01(=dQ10), dQ11, d_opacity,
+ * d_r, d_g, d_b, d_z}.  No atomics: deterministic. */
+typedef struct gs_blend_bwd_args {
+  gs_camera cam;
+  int32_t tiles_x, tiles_y;
+  const uint32_t *ranges;
+  const uint32_t *sorted_gauss;
+  const uint32_t *sorted_pairs; /* [T] entry index e of each sorted entry */
+  const float *records;
+  const float *pix_acc;
+  const float *pix_state;
+  const float *g_image;         /* [3,H,W] dL/dimage */
+  const float *g_alpha;         /* [H,W] or NULL */
+  const float *g_depth;         /* [H,W] or NULL */
+  float *pair_grads;            /* [T, GS_PAIR_GRAD_FLOATS] */
+} gs_blend_bwd_args;
+gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
+
+/* ---- Backward of the projection ----------------------------------------
+ * Sums each Gaussian's pair slots (contiguous: [pair_offset[g],
+ * pair_offset[g] + touches)), adds cotangents on the viewspace_points /
+ * conics outputs, and chains through sigmoid(colour), inv(cov2d),
+ * J cov_cam J^T, Rv Sigma Rv^T, the perspective Jacobian J(X,Y,Z) and
+ * Xc = Rv Xw + Tv (autograd of renderer.py:117-200), and, on the raw path,
+ * through Sigma(exp(s), normalize(q)) (gaussian_model.py:200-207). */
+typedef struct gs_project_bwd_args {
+  gs_camera cam;
+  gs_gaussians g;
+  const float *means2d, *conics;
+  const uint8_t *vis;
+  const uint32_t *rects;
+  const uint32_t *pair_offset;
+  const float *pair_grads;     /* may be NULL when T == 0 */
+  const float *g_means2d;      /* [n,2] or NULL */
+  const float *g_conics;       /* [n,4] or NULL */
+  float *d_xyz;                /* [n,3] */
+  float *d_cov3d;              /* [n,9]  (cov3d path) */
+  float *d_scaling;            /* [n,3]  (raw path)   */
+  float *d_rotation;           /* [n,4]  (raw path)   */
+  float *d_color_logits;       /* [n,3] */
+  float *d_opacity;            /* [n]   */
+} gs_project_bwd_args;
+gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
+
+/* ---- misc --------------------------------------------------------------- */
+int32_t gs_abi_version(void);
+const char *gs_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSPLAT_MI355X_H */

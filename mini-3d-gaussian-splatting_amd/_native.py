@@ -1,0 +1,158 @@
+"""ctypes binding of libgsplat_mi355x.so (the C ABI in include/gsplat_mi355x.h).
+
+The shared library is built in-tree (see build.py) and is the ONLY compute
+path of this package: there is no CPU or eager-PyTorch fallback.  If the
+library is missing, or no HIP device is present, every entry point raises.
+
+torch is imported before the library is opened so that the HIP runtime torch
+already loaded (libamdhip64.so.7) is the one the library binds to.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch  # noqa: F401  (must be loaded before the HIP library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libgsplat_mi355x.so"
+LIB_PATH = os.path.join(_HERE, LIB_NAME)
+
+GS_TILE = 16
+GS_RECORD_FLOATS = 12
+GS_PAIR_GRAD_FLOATS = 10
+GS_NUM_COUNTERS = 4
+GS_ABI_VERSION = 1
+
+_vp = C.c_void_p
+
+
+class GsCamera(C.Structure):
+    _fields_ = [
+        ("image_width", C.c_int32), ("image_height", C.c_int32),
+        ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+        ("view", C.c_float * 12), ("radius_min", C.c_float), ("radius_max", C.c_float),
+        ("bg", C.c_float * 3), ("tile_size", C.c_int32),
+    ]
+
+
+class GsGaussians(C.Structure):
+    _fields_ = [
+        ("n", C.c_int32), ("xyz", _vp), ("xyz_stride", C.c_int64), ("cov3d", _vp),
+        ("scaling", _vp), ("rotation", _vp), ("color_logits", _vp), ("color_stride", C.c_int64),
+        ("opacity", _vp), ("opacity_stride", C.c_int64),
+    ]
+
+
+class GsProjectArgs(C.Structure):
+    _fields_ = [
+        ("cam", GsCamera), ("g", GsGaussians), ("means2d", _vp), ("conics", _vp), ("radii", _vp),
+        ("vis", _vp), ("records", _vp), ("rects", _vp), ("depth_keys", _vp), ("counters", _vp),
+    ]
+
+
+class GsBinArgs(C.Structure):
+    _fields_ = [
+        ("n", C.c_int32), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("sorted_ids", _vp),
+        ("rects", _vp), ("counters", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
+        ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp),
+    ]
+
+
+class GsRangeArgs(C.Structure):
+    _fields_ = [
+        ("num_pairs", C.c_int32), ("num_tiles", C.c_int32), ("sorted_keys", _vp),
+        ("sorted_pairs", _vp), ("pair_gauss", _vp), ("ranges", _vp), ("sorted_gauss", _vp),
+    ]
+
+
+class GsBlendFwdArgs(C.Structure):
+    _fields_ = [
+        ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
+        ("sorted_gauss", _vp), ("records", _vp), ("image", _vp), ("alpha", _vp), ("depth", _vp),
+        ("pix_acc", _vp), ("pix_state", _vp),
+    ]
+
+
+class GsBlendBwdArgs(C.Structure):
+    _fields_ = [
+        ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
+        ("sorted_gauss", _vp), ("sorted_pairs", _vp), ("records", _vp), ("pix_acc", _vp),
+        ("pix_state", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp),
+        ("pair_grads", _vp),
+    ]
+
+
+class GsProjectBwdArgs(C.Structure):
+    _fields_ = [
+        ("cam", GsCamera), ("g", GsGaussians), ("means2d", _vp), ("conics", _vp), ("vis", _vp),
+        ("rects", _vp), ("pair_offset", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
+        ("g_conics", _vp), ("d_xyz", _vp), ("d_cov3d", _vp), ("d_scaling", _vp),
+        ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp),
+    ]
+
+
+# Every symbol the header declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
+    "gs_radix_sort_pairs", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
+    "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
+)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def _declare(lib):
+    P = C.POINTER
+    lib.gs_abi_version.restype = C.c_int32
+    lib.gs_last_error.restype = C.c_char_p
+    lib.gs_project_forward.argtypes = [P(GsProjectArgs), _vp]
+    lib.gs_radix_sort_workspace_bytes.argtypes = [C.c_int32]
+    lib.gs_radix_sort_workspace_bytes.restype = C.c_size_t
+    lib.gs_radix_sort_pairs.argtypes = [_vp, _vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                        _vp, C.c_size_t, P(C.c_int32), _vp]
+    lib.gs_bin_workspace_bytes.argtypes = [C.c_int32]
+    lib.gs_bin_workspace_bytes.restype = C.c_size_t
+    lib.gs_bin_count.argtypes = [P(GsBinArgs), _vp]
+    lib.gs_bin_emit.argtypes = [P(GsBinArgs), _vp]
+    lib.gs_tile_ranges.argtypes = [P(GsRangeArgs), _vp]
+    lib.gs_blend_forward.argtypes = [P(GsBlendFwdArgs), _vp]
+    lib.gs_blend_backward.argtypes = [P(GsBlendBwdArgs), _vp]
+    lib.gs_project_backward.argtypes = [P(GsProjectBwdArgs), _vp]
+    for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_bin_count", "gs_bin_emit",
+              "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward"):
+        getattr(lib, f).restype = C.c_int
+
+
+def load(path: str = LIB_PATH):
+    """Open the HIP library (no device work happens here)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise NativeLibraryError(
+                    f"{LIB_NAME} not found at {path}; build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+            lib = C.CDLL(path)
+            _declare(lib)
+            v = lib.gs_abi_version()
+            if v != GS_ABI_VERSION:
+                raise NativeLibraryError(f"{LIB_NAME} ABI {v} != expected {GS_ABI_VERSION}")
+            _lib = lib
+    return _lib
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = load().gs_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (gs_status={status}): {msg}")
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

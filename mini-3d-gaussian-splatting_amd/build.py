@@ -1,0 +1,45 @@
+"""Builds libgsplat_mi355x.so in-tree with hipcc for gfx950.
+
+    python mini-3d-gaussian-splatting_amd/build.py [--force]
+
+The built .so is git-ignored but travels to the GPU box with the repo
+snapshot (it is not in .gpurunignore).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = [os.path.join(HERE, "csrc", "gsplat_mi355x.hip")]
+HDR = [os.path.join(ROOT, "include", "gsplat_mi355x.h")]
+OUT = os.path.join(HERE, "libgsplat_mi355x.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+         # the blend's skip/termination decisions must replay bit-identically
+         # between forward and backward, and follow the reference's unfused
+         # fp32 order; no contraction of a*b+c into fma.
+         "-ffp-contract=off",
+         "-Wall", "-Wno-unused-function"]
+
+
+def stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(p) > t for p in SRC + HDR + [__file__])
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if force or stale():
+        cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), *SRC, "-o", OUT]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,998 @@
+// gsplat_mi355x.hip -- CDNA4 (gfx950) kernels behind include/gsplat_mi355x.h.
+//
+// Differentiable tile rasterizer replacing GaussianRenderer.render() of the
+// reference (src/core/renderer.py:31-367) and its autograd backward.
+// Stages (each cites the reference lines it replaces):
+//   k_project_fwd     renderer.py:117-220   projection, 2D cov, conic, radius, culling
+//   k_radix_*         renderer.py:231-237   stable LSD radix sort (depth, then tile id)
+//   k_bin_*           renderer.py:263-298   tile binning, emitted in depth order
+//   k_tile_ranges     renderer.py:266       per-tile list ranges
+//   k_blend_fwd       renderer.py:273-367   per-pixel front-to-back compositing
+//   k_blend_bwd       autograd of :313-367  replayed front-to-back, per-pair grad slots
+//   k_project_bwd     autograd of :117-200  (+ gaussian_model.py:200-207 on the raw path)
+//
+// Layout and roofline notes: DESIGN.md.  Wave size is 64 everywhere.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "gsplat_mi355x.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWave = 64;
+constexpr int kRadixBits = 8;
+constexpr int kRadix = 1 << kRadixBits;
+constexpr int kSortIpt = 16;                     // items per thread per sort block
+constexpr int kSortChunk = kBlock * kSortIpt;    // 4096 items per block
+constexpr int kBinChunk = kBlock * 16;           // 4096 Gaussians per binning block
+constexpr float kAlphaStop = 0.995f;             // renderer.py:352
+constexpr float kMinWeight = 1e-5f;              // renderer.py:336
+
+thread_local char g_err[512];
+
+gs_status fail(gs_status s, const char *fmt, const char *what) {
+  snprintf(g_err, sizeof(g_err), fmt, what);
+  return s;
+}
+
+gs_status check_launch(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: launch failed: %s", what, hipGetErrorString(e));
+    return GS_ERR_LAUNCH;
+  }
+  return GS_OK;
+}
+
+inline unsigned div_up(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
+// torch.clamp semantics (NaN propagates)
+__device__ __forceinline__ float clamp01(float v) { return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
+__device__ __forceinline__ float clampf(float v, float lo, float hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  const int lane = threadIdx.x & (kWave - 1);
+  return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+}
+
+// ---------------------------------------------------------------- scans ----
+// Exclusive scan of one u32 per thread over a 256-thread block.
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *s_tmp, uint32_t *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) s_tmp[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) {
+    uint32_t x = s_tmp[w];
+    base += (w < wave) ? x : 0u;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+// Lanes of the wave holding the same `nbits`-bit digit (match-any via ballots).
+__device__ __forceinline__ unsigned long long match_digit(uint32_t d, int nbits, unsigned long long m) {
+  for (int b = 0; b < nbits; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const unsigned long long bb = __ballot(bit);
+    m &= bit ? bb : ~bb;
+  }
+  return m;
+}
+
+// ------------------------------------------------------ wave reductions ----
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// Sum over the 64 lanes; every lane must be active.  Row sums via DPP
+// (quad_perm, row_ror), then the four row totals via readlane.
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x124>(v);  // row_ror:4
+  v += dpp<0x128>(v);  // row_ror:8
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
+// ------------------------------------------------------------ geometry ----
+__device__ __forceinline__ void unpack_rect(const uint32_t *rects, uint32_t g, int &tx0, int &tx1,
+                                            int &ty0, int &ty1) {
+  const uint2 r = reinterpret_cast<const uint2 *>(rects)[g];
+  tx0 = (int)(r.x & 0xFFFFu);
+  tx1 = (int)(r.x >> 16);
+  ty0 = (int)(r.y & 0xFFFFu);
+  ty1 = (int)(r.y >> 16);
+}
+__device__ __forceinline__ uint32_t rect_touches(int tx0, int tx1, int ty0, int ty1) {
+  return (tx1 >= tx0 && ty1 >= ty0) ? (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1)) : 0u;
+}
+
+// Sigma = R(normalize(q)) diag(exp(s)^2) R^T  (gaussian_model.py:200-207,
+// math_utils.py:10-26), fp32 in the reference's order.
+__device__ __forceinline__ void cov_from_raw(const float *sc, const float *rq, float S[9]) {
+  float w = rq[0], x = rq[1], y = rq[2], z = rq[3];
+  for (int it = 0; it < 2; ++it) {  // get_rotation normalises, build_rotation_matrix again
+    float n = sqrtf(w * w + x * x + y * y + z * z);
+    n = n < 1e-12f ? 1e-12f : n;
+    w /= n; x /= n; y /= n; z /= n;
+  }
+  const float R[9] = {1.f - 2.f * (y * y + z * z), 2.f * (x * y - w * z), 2.f * (x * z + w * y),
+                      2.f * (x * y + w * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - w * x),
+                      2.f * (x * z - w * y), 2.f * (y * z + w * x), 1.f - 2.f * (x * x + y * y)};
+  float s2[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float s = expf(sc[k]);
+    s2[k] = s * s;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      S[i * 3 + j] = ((R[i * 3] * s2[0]) * R[j * 3] + (R[i * 3 + 1] * s2[1]) * R[j * 3 + 1]) +
+                     (R[i * 3 + 2] * s2[2]) * R[j * 3 + 2];
+}
+
+// =================================================== stage 1: projection ==
+__global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
+  const int g = blockIdx.x * kBlock + threadIdx.x;
+  bool visible = false;
+  if (g < a.g.n) {
+    const gs_camera &c = a.cam;
+    const float *X3 = a.g.xyz + (int64_t)g * a.g.xyz_stride;
+    const float xw = X3[0], yw = X3[1], zw = X3[2];
+    float S[9];
+    if (a.g.cov3d) {
+      const float *cp = a.g.cov3d + (int64_t)g * 9;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) S[k] = cp[k];
+    } else {
+      cov_from_raw(a.g.scaling + (int64_t)g * 3, a.g.rotation + (int64_t)g * 4, S);
+    }
+    const float *R = c.view;  // rows [R | t]
+    // Xc = Xw @ Rv.T + Tv (renderer.py:154)
+    float Xc[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      Xc[i] = ((xw * R[i * 4] + yw * R[i * 4 + 1]) + zw * R[i * 4 + 2]) + R[i * 4 + 3];
+    const float X = Xc[0], Y = Xc[1], Z = Xc[2];
+    const float mx = (c.fx * X) / Z + c.cx;      // :161
+    const float my = ((-c.fy) * Y) / Z + c.cy;   // :162
+    // cov_cam = (Rv @ Sigma) @ Rv.T (:168)
+    float RS[9], C[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        RS[i * 3 + j] = (R[i * 4] * S[j] + R[i * 4 + 1] * S[3 + j]) + R[i * 4 + 2] * S[6 + j];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        C[i * 3 + j] = (RS[i * 3] * R[j * 4] + RS[i * 3 + 1] * R[j * 4 + 1]) + RS[i * 3 + 2] * R[j * 4 + 2];
+    // J (:171-177)
+    const float iz = 1.0f / Z;
+    const float J[6] = {c.fx * iz, 0.f, (((-c.fx) * X) * iz) * iz, 0.f, (-c.fy) * iz, ((c.fy * Y) * iz) * iz};
+    float JC[6];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        JC[i * 3 + j] = (J[i * 3] * C[j] + J[i * 3 + 1] * C[3 + j]) + J[i * 3 + 2] * C[6 + j];
+    float V[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        V[i * 2 + j] = (JC[i * 3] * J[j * 3] + JC[i * 3 + 1] * J[j * 3 + 1]) + JC[i * 3 + 2] * J[j * 3 + 2];
+    V[0] += 1e-6f;  // :182-183
+    V[3] += 1e-6f;
+    // conic = inv(cov2d) (:186) and lambda_max (:188) in double: LAPACK-grade
+    const double va = V[0], vb = V[1], vc = V[2], vd = V[3];
+    const double det = va * vd - vb * vc;
+    const float q0 = (float)(vd / det), q1 = (float)(-vb / det), q2 = (float)(-vc / det),
+                q3 = (float)(va / det);
+    const double hm = 0.5 * (va + vd), hd = 0.5 * (va - vd);
+    const float lmax = (float)(hm + sqrt(hd * hd + vc * vc));
+    const float r = clampf(3.0f * sqrtf(lmax), c.radius_min, c.radius_max);  // :190-192
+    const int W = c.image_width, H = c.image_height;
+    // culling (:218)
+    visible = (Z > 0.f) && (mx >= -r) && (mx < (float)W + r) && (my >= -r) && (my < (float)H + r) &&
+              (r > 0.f);
+    reinterpret_cast<float2 *>(a.means2d)[g] = make_float2(mx, my);
+    reinterpret_cast<float4 *>(a.conics)[g] = make_float4(q0, q1, q2, q3);
+    a.radii[g] = r;
+    a.vis[g] = visible ? 1 : 0;
+    // tile rectangle (:278-293), int() truncation toward zero
+    uint32_t rx = 1u, ry = 1u;  // empty: tx0=1 > tx1=0
+    if (visible) {
+      const int ri = (int)r, icx = (int)mx, icy = (int)my;
+      int x0 = icx - ri, x1 = icx + 1 + ri, y0 = icy - ri, y1 = icy + 1 + ri;
+      x0 = x0 < 0 ? 0 : x0;
+      y0 = y0 < 0 ? 0 : y0;
+      x1 = x1 > W ? W : x1;
+      y1 = y1 > H ? H : y1;
+      if (x0 < x1 && y0 < y1) {
+        const int T = GS_TILE;
+        rx = (uint32_t)(x0 / T) | ((uint32_t)((x1 - 1) / T) << 16);
+        ry = (uint32_t)(y0 / T) | ((uint32_t)((y1 - 1) / T) << 16);
+      }
+      const float *cl = a.g.color_logits + (int64_t)g * a.g.color_stride;
+      const float op = a.g.opacity[(int64_t)g * a.g.opacity_stride];
+      float4 *rec = reinterpret_cast<float4 *>(a.records) + 3 * (int64_t)g;
+      rec[0] = make_float4(mx, my, q0, q1 + q2);
+      rec[1] = make_float4(q3, op, Z, 0.f);
+      rec[2] = make_float4(1.f / (1.f + expf(-cl[0])), 1.f / (1.f + expf(-cl[1])),
+                           1.f / (1.f + expf(-cl[2])), 0.f);  // sigmoid (:90)
+    }
+    reinterpret_cast<uint2 *>(a.rects)[g] = make_uint2(rx, ry);
+    a.depth_keys[g] = visible ? __float_as_uint(Z) : 0xFFFFFFFFu;
+  }
+  const unsigned long long b = __ballot(visible);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&a.counters[0], (uint32_t)__popcll(b));
+}
+
+// ===================================================== radix sort =========
+// Pass p sorts digit (key >> shift) & mask.  One block = kSortChunk items;
+// wave w owns the contiguous quarter [w*1024, (w+1)*1024) of the chunk,
+// walked in 16 rounds of 64 (order = wave, round, lane: stable).
+__global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restrict__ keys, int n, int shift,
+                                                       int nbits, uint32_t *counts, uint32_t *digit_total,
+                                                       int nb) {
+  __shared__ uint32_t hist[kRadix];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t mask = (1u << nbits) - 1u;
+  const long long base = (long long)blockIdx.x * kSortChunk + wave * (kSortChunk / 4);
+  for (int r = 0; r < kSortIpt; ++r) {
+    const long long idx = base + r * 64 + lane;
+    const bool valid = idx < n;
+    const uint32_t d = valid ? ((keys[idx] >> shift) & mask) : 0u;
+    const unsigned long long m = match_digit(d, nbits, __ballot(valid));
+    if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(m));
+  }
+  __syncthreads();
+  const uint32_t h = hist[threadIdx.x];
+  counts[(size_t)threadIdx.x * nb + blockIdx.x] = h;
+  if (h) atomicAdd(&digit_total[threadIdx.x], h);
+}
+
+// counts[d][b] -> global exclusive offsets; one block per digit.
+__global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, const uint32_t *digit_total, int nb) {
+  __shared__ uint32_t s_tmp[4];
+  const int d = blockIdx.x;
+  uint32_t tot;
+  const uint32_t mine = threadIdx.x < (unsigned)d ? digit_total[threadIdx.x] : 0u;
+  const uint32_t ex = block_exscan(mine, s_tmp, &tot);
+  (void)ex;
+  uint32_t carry = tot;  // sum of totals of digits < d
+  uint32_t *row = counts + (size_t)d * nb;
+  for (int c = 0; c < nb; c += kBlock) {
+    const int i = c + threadIdx.x;
+    const uint32_t v = i < nb ? row[i] : 0u;
+    const uint32_t e = block_exscan(v, s_tmp, &tot);
+    if (i < nb) row[i] = carry + e;
+    carry += tot;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
+                                                          const uint32_t *__restrict__ vals_in,
+                                                          uint32_t *__restrict__ keys_out,
+                                                          uint32_t *__restrict__ vals_out, int n, int shift,
+                                                          int nbits, const uint32_t *counts, int nb) {
+  __shared__ uint32_t wcnt[4][kRadix];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t mask = (1u << nbits) - 1u;
+  const long long base = (long long)blockIdx.x * kSortChunk + wave * (kSortChunk / 4);
+  uint32_t k_[kSortIpt], v_[kSortIpt], rk[kSortIpt];
+#pragma unroll
+  for (int r = 0; r < kSortIpt; ++r) {
+    const long long idx = base + r * 64 + lane;
+    const bool valid = idx < n;
+    const uint32_t key = valid ? keys_in[idx] : 0u;
+    const uint32_t val = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+    const uint32_t d = (key >> shift) & mask;
+    const unsigned long long m = match_digit(d, nbits, __ballot(valid));
+    const uint32_t below = (uint32_t)__popcll(m & lanemask_lt());
+    uint32_t old = 0;
+    if (valid) old = wcnt[wave][d];
+    if (valid && below == 0) wcnt[wave][d] = old + (uint32_t)__popcll(m);
+    k_[r] = key;
+    v_[r] = val;
+    rk[r] = valid ? old + below : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  {
+    uint32_t run = counts[(size_t)threadIdx.x * nb + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t t = wcnt[w][threadIdx.x];
+      wcnt[w][threadIdx.x] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSortIpt; ++r) {
+    if (rk[r] != 0xFFFFFFFFu) {
+      const uint32_t d = (k_[r] >> shift) & mask;
+      const uint32_t dst = wcnt[wave][d] + rk[r];
+      keys_out[dst] = k_[r];
+      vals_out[dst] = v_[r];
+    }
+  }
+}
+
+// ======================================================== binning =========
+__global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials) {
+  __shared__ uint32_t s_tmp[4];
+  const long long base = (long long)blockIdx.x * kBinChunk;
+  uint32_t sum = 0;
+  for (int i = 0; i < kBinChunk / kBlock; ++i) {
+    const long long k = base + i * kBlock + threadIdx.x;
+    if (k < a.n) {
+      int tx0, tx1, ty0, ty1;
+      unpack_rect(a.rects, a.sorted_ids[k], tx0, tx1, ty0, ty1);
+      sum += rect_touches(tx0, tx1, ty0, ty1);
+    }
+  }
+  uint32_t tot;
+  block_exscan(sum, s_tmp, &tot);
+  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+// exclusive scan of the block partials (single block); counters[1] = T
+__global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials, int nb, uint32_t *counters) {
+  __shared__ uint32_t s_tmp[4];
+  uint32_t carry = 0, tot;
+  for (int c = 0; c < nb; c += kBlock) {
+    const int i = c + threadIdx.x;
+    const uint32_t v = i < nb ? partials[i] : 0u;
+    const uint32_t e = block_exscan(v, s_tmp, &tot);
+    if (i < nb) partials[i] = carry + e;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) counters[1] = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials) {
+  __shared__ uint32_t s_ids[kBinChunk];
+  __shared__ uint32_t s_tmp[4];
+  const long long base = (long long)blockIdx.x * kBinChunk;
+  for (int i = 0; i < kBinChunk / kBlock; ++i) {
+    const long long k = base + i * kBlock + threadIdx.x;
+    s_ids[i * kBlock + threadIdx.x] = k < a.n ? a.sorted_ids[k] : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  constexpr int per = kBinChunk / kBlock;  // 16 consecutive items per thread
+  uint32_t cnt[per];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < per; ++j) {
+    const uint32_t g = s_ids[threadIdx.x * per + j];
+    uint32_t t = 0;
+    if (g != 0xFFFFFFFFu) {
+      int tx0, tx1, ty0, ty1;
+      unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
+      t = rect_touches(tx0, tx1, ty0, ty1);
+    }
+    cnt[j] = t;
+    sum += t;
+  }
+  uint32_t tot;
+  uint32_t off = block_exscan(sum, s_tmp, &tot) + partials[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < per; ++j) {
+    const uint32_t g = s_ids[threadIdx.x * per + j];
+    if (g == 0xFFFFFFFFu) continue;
+    a.pair_offset[g] = off;
+    if (cnt[j]) {
+      int tx0, tx1, ty0, ty1;
+      unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
+      for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+          a.tile_keys[off] = (uint32_t)(ty * a.tiles_x + tx);
+          a.pair_gauss[off] = g;
+          ++off;
+        }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
+  const long long p = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= a.num_pairs) return;
+  const uint32_t t = a.sorted_keys[p];
+  if (p == 0 || a.sorted_keys[p - 1] != t) a.ranges[2 * t] = (uint32_t)p;
+  if (p == a.num_pairs - 1 || a.sorted_keys[p + 1] != t) a.ranges[2 * t + 1] = (uint32_t)(p + 1);
+  a.sorted_gauss[p] = a.pair_gauss[a.sorted_pairs[p]];
+}
+
+// ======================================================== blend fwd =======
+// Pixel of thread tid in its 16x16 tile: wave w covers the 8x8 quadrant
+// (w&1, w>>1), lane l the pixel (l&7, l>>3) of it -- compact footprints per
+// wave keep the per-pair branches coherent.
+__device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int &px, int &py) {
+  const int tx = tile % tiles_x, ty = tile / tiles_x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  px = tx * GS_TILE + ((wave & 1) << 3) + (lane & 7);
+  py = ty * GS_TILE + ((wave >> 1) << 3) + (lane >> 3);
+}
+
+__global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
+  __shared__ float4 s_r0[kBlock], s_r1[kBlock], s_r2[kBlock];
+  const int tile = blockIdx.x;
+  int px, py;
+  tile_pixel(tile, a.tiles_x, px, py);
+  const int W = a.cam.image_width, H = a.cam.image_height;
+  const bool inside = px < W && py < H;
+  const uint32_t start = a.ranges[2 * tile], end = a.ranges[2 * tile + 1];
+  const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
+  float ar = bg0, ag = bg1, ab = bg2;  // out_rgb = bg (renderer.py:273)
+  float A = 0.f, D = 0.f;
+  bool done = !inside;
+  uint32_t neval = 0;
+  const float fx = (float)px, fy = (float)py;
+  const float4 *recs = reinterpret_cast<const float4 *>(a.records);
+  for (uint32_t b = start; b < end; b += kBlock) {
+    const uint32_t cnt = min((uint32_t)kBlock, end - b);
+    if (threadIdx.x < cnt) {
+      const uint32_t gid = a.sorted_gauss[b + threadIdx.x];
+      s_r0[threadIdx.x] = recs[3 * (size_t)gid];
+      s_r1[threadIdx.x] = recs[3 * (size_t)gid + 1];
+      s_r2[threadIdx.x] = recs[3 * (size_t)gid + 2];
+    }
+    __syncthreads();
+    if (!done) {
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const float4 r0 = s_r0[j];
+        const float4 r1 = s_r1[j];
+        const float dx = fx - r0.x, dy = fy - r0.y;
+        const float s = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;  // :333
+        const float w = clamp01(expf(-0.5f * s));                                 // :334
+        if (w < kMinWeight) continue;                                            // :336
+        const float ai = clamp01(r1.y * w);                                      // :339
+        if (ai <= 0.f) continue;
+        const float c = (1.f - A) * ai;                                          // :343-344
+        if (c <= 0.f) continue;
+        const float4 r2 = s_r2[j];
+        ar += c * r2.x;
+        ag += c * r2.y;
+        ab += c * r2.z;
+        A = A + c;
+        D += c * r1.z;
+        if (A >= kAlphaStop) {  // :352 (after accumulation)
+          done = true;
+          neval = b - start + j + 1;
+          break;
+        }
+      }
+    }
+    if (__syncthreads_count(done) == kBlock) break;
+  }
+  if (!inside) return;
+  if (!done) neval = end - start;
+  const size_t HW = (size_t)W * H, p = (size_t)py * W + px;
+  const float tb = 1.f - A;
+  a.image[p] = clamp01(ar + tb * bg0);  // :359,364
+  a.image[HW + p] = clamp01(ag + tb * bg1);
+  a.image[2 * HW + p] = clamp01(ab + tb * bg2);
+  a.alpha[p] = clamp01(A);
+  a.depth[p] = D / (A + 1e-6f);  // :362
+  reinterpret_cast<float4 *>(a.pix_acc)[p] = make_float4(ar, ag, ab, D);
+  reinterpret_cast<float2 *>(a.pix_state)[p] = make_float2(A, __uint_as_float(neval));
+}
+
+// ======================================================== blend bwd =======
+__global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
+  __shared__ float4 s_r0[kBlock], s_r1[kBlock], s_r2[kBlock];
+  __shared__ uint32_t s_e[kBlock];
+  __shared__ float s_red[4][kBlock * GS_PAIR_GRAD_FLOATS];
+  __shared__ uint32_t s_max;
+  const int tile = blockIdx.x;
+  int px, py;
+  tile_pixel(tile, a.tiles_x, px, py);
+  const int W = a.cam.image_width, H = a.cam.image_height;
+  const bool inside = px < W && py < H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t start = a.ranges[2 * tile], end = a.ranges[2 * tile + 1];
+  const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
+  if (threadIdx.x == 0) s_max = 0;
+  // pixel cotangents through clamp / bg composite / depth normalisation
+  float gR0 = 0.f, gR1 = 0.f, gR2 = 0.f, gA = 0.f, gD = 0.f;
+  float tr = 0.f, tg = 0.f, tbl = 0.f, Dt = 0.f, At = 0.f;
+  uint32_t neval = 0;
+  const size_t HW = (size_t)W * H;
+  if (inside) {
+    const size_t p = (size_t)py * W + px;
+    const float4 acc = reinterpret_cast<const float4 *>(a.pix_acc)[p];
+    const float2 st = reinterpret_cast<const float2 *>(a.pix_state)[p];
+    tr = acc.x; tg = acc.y; tbl = acc.z; Dt = acc.w; At = st.x;
+    neval = __float_as_uint(st.y);
+    const float tb = 1.f - At;
+    const float pr = tr + tb * bg0, pg = tg + tb * bg1, pb = tbl + tb * bg2;
+    gR0 = (pr >= 0.f && pr <= 1.f) ? a.g_image[p] : 0.f;
+    gR1 = (pg >= 0.f && pg <= 1.f) ? a.g_image[HW + p] : 0.f;
+    gR2 = (pb >= 0.f && pb <= 1.f) ? a.g_image[2 * HW + p] : 0.f;
+    gA = -gR0 * bg0 - gR1 * bg1 - gR2 * bg2;
+    if (a.g_alpha && At >= 0.f && At <= 1.f) gA += a.g_alpha[p];
+    if (a.g_depth) {
+      const float den = At + 1e-6f;
+      gD = a.g_depth[p] / den;
+      gA += -a.g_depth[p] * Dt / (den * den);
+    }
+  }
+  __syncthreads();
+  if (neval) atomicMax(&s_max, neval);
+  __syncthreads();
+  const uint32_t stop = start + s_max;
+  const float fx = (float)px, fy = (float)py;
+  const float onemA = 1.f - At;
+  float A = 0.f, D = 0.f, ar = bg0, ag = bg1, ab = bg2;
+  const float4 *recs = reinterpret_cast<const float4 *>(a.records);
+  for (uint32_t b = start; b < stop; b += kBlock) {
+    const uint32_t cnt = min((uint32_t)kBlock, stop - b);
+    __syncthreads();  // previous batch's s_red / records consumed
+    if (threadIdx.x < cnt) {
+      const uint32_t gid = a.sorted_gauss[b + threadIdx.x];
+      s_r0[threadIdx.x] = recs[3 * (size_t)gid];
+      s_r1[threadIdx.x] = recs[3 * (size_t)gid + 1];
+      s_r2[threadIdx.x] = recs[3 * (size_t)gid + 2];
+      s_e[threadIdx.x] = a.sorted_pairs[b + threadIdx.x];
+    }
+    __syncthreads();
+    const uint32_t jbase = b - start;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      float gv[GS_PAIR_GRAD_FLOATS];
+#pragma unroll
+      for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) gv[k] = 0.f;
+      bool contributed = false;
+      if (jbase + j < neval) {
+        const float4 r0 = s_r0[j];
+        const float4 r1 = s_r1[j];
+        const float dx = fx - r0.x, dy = fy - r0.y;
+        const float s = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;
+        const float e = expf(-0.5f * s);
+        const float w = clamp01(e);
+        if (w >= kMinWeight) {
+          const float u = r1.y * w;
+          const float ai = clamp01(u);
+          if (ai > 0.f) {
+            const float trans = 1.f - A;
+            const float c = trans * ai;
+            if (c > 0.f) {
+              contributed = true;
+              const float4 r2 = s_r2[j];
+              ar += c * r2.x;
+              ag += c * r2.y;
+              ab += c * r2.z;
+              A = A + c;
+              D += c * r1.z;
+              const float Tn = 1.f - A;
+              float dal;
+              if (Tn == 0.f) {
+                dal = trans * (gR0 * r2.x + gR1 * r2.y + gR2 * r2.z + gD * r1.z + gA);
+              } else {
+                const float inv = 1.f / Tn;
+                const float sr = gR0 * (r2.x - (tr - ar) * inv) + gR1 * (r2.y - (tg - ag) * inv) +
+                                 gR2 * (r2.z - (tbl - ab) * inv) + gD * (r1.z - (Dt - D) * inv) +
+                                 gA * (onemA * inv);
+                dal = trans * sr;
+              }
+              const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
+              const float dw = du * r1.y;
+              const float de = (e >= 0.f && e <= 1.f) ? dw : 0.f;
+              const float ds = de * e * -0.5f;
+              gv[0] = -ds * (2.f * dx * r0.z + r0.w * dy);
+              gv[1] = -ds * (r0.w * dx + 2.f * dy * r1.x);
+              gv[2] = ds * dx * dx;
+              gv[3] = ds * dx * dy;
+              gv[4] = ds * dy * dy;
+              gv[5] = du * w;
+              gv[6] = gR0 * c;
+              gv[7] = gR1 * c;
+              gv[8] = gR2 * c;
+              gv[9] = gD * c;
+            }
+          }
+        }
+      }
+      float *dst = &s_red[wave][j * GS_PAIR_GRAD_FLOATS];
+      if (__any(contributed)) {
+#pragma unroll
+        for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) {
+          const float v = wave_sum(gv[k]);
+          if (lane == 0) dst[k] = v;
+        }
+      } else if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) dst[k] = 0.f;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < cnt) {
+      const int j = threadIdx.x;
+      float *out = a.pair_grads + (size_t)s_e[j] * GS_PAIR_GRAD_FLOATS;
+#pragma unroll
+      for (int k = 0; k < GS_PAIR_GRAD_FLOATS; k += 2) {
+        const int o = j * GS_PAIR_GRAD_FLOATS + k;
+        const float v0 = (s_red[0][o] + s_red[1][o]) + (s_red[2][o] + s_red[3][o]);
+        const float v1 = (s_red[0][o + 1] + s_red[1][o + 1]) + (s_red[2][o + 1] + s_red[3][o + 1]);
+        reinterpret_cast<float2 *>(out)[k / 2] = make_float2(v0, v1);
+      }
+    }
+  }
+  // entries past every pixel's last evaluated pair carry no gradient
+  for (uint32_t q = stop + threadIdx.x; q < end; q += kBlock) {
+    float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)a.sorted_pairs[q] * GS_PAIR_GRAD_FLOATS);
+#pragma unroll
+    for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) out[k] = make_float2(0.f, 0.f);
+  }
+}
+
+// ======================================================== project bwd =====
+__global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
+  const int g = blockIdx.x * kBlock + threadIdx.x;
+  if (g >= a.g.n) return;
+  float acc[GS_PAIR_GRAD_FLOATS];
+#pragma unroll
+  for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
+  if (a.vis[g] && a.pair_grads) {
+    int tx0, tx1, ty0, ty1;
+    unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
+    const uint32_t cnt = rect_touches(tx0, tx1, ty0, ty1);
+    const uint32_t off = a.pair_offset[g];
+    for (uint32_t e = off; e < off + cnt; ++e) {
+      const float2 *sl = reinterpret_cast<const float2 *>(a.pair_grads + (size_t)e * GS_PAIR_GRAD_FLOATS);
+#pragma unroll
+      for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) {
+        const float2 v = sl[k];
+        acc[2 * k] += v.x;
+        acc[2 * k + 1] += v.y;
+      }
+    }
+  }
+  double dm0 = acc[0], dm1 = acc[1];
+  double G[4] = {acc[2], acc[3], acc[3], acc[4]};
+  if (a.g_means2d) {
+    dm0 += a.g_means2d[2 * (size_t)g];
+    dm1 += a.g_means2d[2 * (size_t)g + 1];
+  }
+  if (a.g_conics) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) G[k] += a.g_conics[4 * (size_t)g + k];
+  }
+  // colour: sigmoid chain (renderer.py:90)
+  const float *cl = a.g.color_logits + (int64_t)g * a.g.color_stride;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float c = 1.f / (1.f + expf(-cl[k]));
+    a.d_color_logits[3 * (size_t)g + k] = acc[6 + k] * c * (1.f - c);
+  }
+  a.d_opacity[g] = acc[5];
+  const bool any = dm0 != 0.0 || dm1 != 0.0 || G[0] != 0.0 || G[1] != 0.0 || G[2] != 0.0 ||
+                   G[3] != 0.0 || acc[9] != 0.f;
+  const bool raw = a.g.cov3d == nullptr;
+  if (!any) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a.d_xyz[3 * (size_t)g + k] = 0.f;
+    if (raw) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a.d_scaling[3 * (size_t)g + k] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a.d_rotation[4 * (size_t)g + k] = 0.f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) a.d_cov3d[9 * (size_t)g + k] = 0.f;
+    }
+    return;
+  }
+  const gs_camera &c = a.cam;
+  const float *R = c.view;
+  const float *X3 = a.g.xyz + (int64_t)g * a.g.xyz_stride;
+  float Sf[9];
+  if (!raw) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Sf[k] = a.g.cov3d[9 * (size_t)g + k];
+  } else {
+    cov_from_raw(a.g.scaling + (int64_t)g * 3, a.g.rotation + (int64_t)g * 4, Sf);
+  }
+  double Xc[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    Xc[i] = (double)X3[0] * R[i * 4] + (double)X3[1] * R[i * 4 + 1] + (double)X3[2] * R[i * 4 + 2] + R[i * 4 + 3];
+  const double X = Xc[0], Y = Xc[1], Z = Xc[2];
+  const double fx = c.fx, fy = c.fy;
+  double RS[9], C[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      RS[i * 3 + j] = (double)R[i * 4] * Sf[j] + (double)R[i * 4 + 1] * Sf[3 + j] + (double)R[i * 4 + 2] * Sf[6 + j];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C[i * 3 + j] = RS[i * 3] * R[j * 4] + RS[i * 3 + 1] * R[j * 4 + 1] + RS[i * 3 + 2] * R[j * 4 + 2];
+  const double iz = 1.0 / Z;
+  const double J[6] = {fx * iz, 0.0, -fx * X * iz * iz, 0.0, -fy * iz, fy * Y * iz * iz};
+  const float4 Qf = reinterpret_cast<const float4 *>(a.conics)[g];
+  const double Q[4] = {Qf.x, Qf.y, Qf.z, Qf.w};
+  // d cov2d = -Q^T G Q^T (inverse backward)
+  const double QG0 = Q[0] * G[0] + Q[2] * G[2], QG1 = Q[0] * G[1] + Q[2] * G[3];
+  const double QG2 = Q[1] * G[0] + Q[3] * G[2], QG3 = Q[1] * G[1] + Q[3] * G[3];
+  const double dV[4] = {-(QG0 * Q[0] + QG1 * Q[1]), -(QG0 * Q[2] + QG1 * Q[3]), -(QG2 * Q[0] + QG3 * Q[1]),
+                        -(QG2 * Q[2] + QG3 * Q[3])};
+  double JCt[6], JCn[6];  // J C^T, J C
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      JCt[i * 3 + j] = J[i * 3] * C[j * 3] + J[i * 3 + 1] * C[j * 3 + 1] + J[i * 3 + 2] * C[j * 3 + 2];
+      JCn[i * 3 + j] = J[i * 3] * C[j] + J[i * 3 + 1] * C[3 + j] + J[i * 3 + 2] * C[6 + j];
+    }
+  double dJ[6];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      dJ[i * 3 + j] = dV[i * 2] * JCt[j] + dV[i * 2 + 1] * JCt[3 + j] + dV[i] * JCn[j] + dV[2 + i] * JCn[3 + j];
+  double dC[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int l = 0; l < 2; ++l) v += J[k * 3 + i] * dV[k * 2 + l] * J[l * 3 + j];
+      dC[i * 3 + j] = v;
+    }
+  double dS[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int l = 0; l < 3; ++l) v += (double)R[k * 4 + i] * dC[k * 3 + l] * R[l * 4 + j];
+      dS[i * 3 + j] = v;
+    }
+  const double iz2 = iz * iz, iz3 = iz2 * iz;
+  const double dX = dm0 * fx * iz + dJ[2] * (-fx * iz2);
+  const double dY = dm1 * (-fy * iz) + dJ[5] * (fy * iz2);
+  const double dZ = dm0 * (-fx * X * iz2) + dm1 * (fy * Y * iz2) + dJ[0] * (-fx * iz2) +
+                    dJ[2] * (2.0 * fx * X * iz3) + dJ[4] * (fy * iz2) + dJ[5] * (-2.0 * fy * Y * iz3) +
+                    (double)acc[9];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    a.d_xyz[3 * (size_t)g + j] = (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ);
+  if (!raw) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a.d_cov3d[9 * (size_t)g + k] = (float)dS[k];
+    return;
+  }
+  // raw path: Sigma = M M^T, M = R(q) diag(s), s = exp(scaling), q = normalize(rotation)
+  const float *sc = a.g.scaling + (int64_t)g * 3, *rq = a.g.rotation + (int64_t)g * 4;
+  double qn = sqrt((double)rq[0] * rq[0] + (double)rq[1] * rq[1] + (double)rq[2] * rq[2] + (double)rq[3] * rq[3]);
+  qn = qn < 1e-12 ? 1e-12 : qn;
+  const double w = rq[0] / qn, x = rq[1] / qn, y = rq[2] / qn, z = rq[3] / qn;
+  const double Rq[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                        2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                        2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
+  const double s[3] = {exp((double)sc[0]), exp((double)sc[1]), exp((double)sc[2])};
+  double dM[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) v += (dS[i * 3 + k] + dS[k * 3 + i]) * Rq[k * 3 + j] * s[j];
+      dM[i * 3 + j] = v;
+    }
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    a.d_scaling[3 * (size_t)g + j] =
+        (float)((dM[j] * Rq[j] + dM[3 + j] * Rq[3 + j] + dM[6 + j] * Rq[6 + j]) * s[j]);
+  double dR[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) dR[i] = dM[i] * s[i % 3];
+  const double dw = 2 * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
+  const double dx = 2 * (y * dR[1] + z * dR[2] + y * dR[3] - 2 * x * dR[4] - w * dR[5] + z * dR[6] + w * dR[7] -
+                         2 * x * dR[8]);
+  const double dy = 2 * (-2 * y * dR[0] + x * dR[1] + w * dR[2] + x * dR[3] + z * dR[5] - w * dR[6] + z * dR[7] -
+                         2 * y * dR[8]);
+  const double dz = 2 * (-2 * z * dR[0] - w * dR[1] + x * dR[2] + w * dR[3] - 2 * z * dR[4] + y * dR[5] +
+                         x * dR[6] + y * dR[7]);
+  const double dot = dw * w + dx * x + dy * y + dz * z;
+  a.d_rotation[4 * (size_t)g + 0] = (float)((dw - w * dot) / qn);
+  a.d_rotation[4 * (size_t)g + 1] = (float)((dx - x * dot) / qn);
+  a.d_rotation[4 * (size_t)g + 2] = (float)((dy - y * dot) / qn);
+  a.d_rotation[4 * (size_t)g + 3] = (float)((dz - z * dot) / qn);
+}
+
+bool cam_ok(const gs_camera &c) {
+  return c.tile_size == GS_TILE && c.image_width > 0 && c.image_height > 0 &&
+         c.image_width < (GS_TILE << 16) && c.image_height < (GS_TILE << 16);
+}
+
+struct SortWs {
+  uint32_t *counts;
+  uint32_t *digit_total;
+};
+
+}  // namespace
+
+// ============================================================ C ABI =======
+extern "C" {
+
+int32_t gs_abi_version(void) { return GS_ABI_VERSION; }
+
+const char *gs_last_error(void) { return g_err; }
+
+gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream) {
+  if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_project_forward");
+  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16 and image size positive", "gs_project_forward");
+  if (a->g.n < 0 || !a->counters) return fail(GS_ERR_INVALID_ARG, "%s: bad n / counters", "gs_project_forward");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(a->counters, 0, sizeof(uint32_t) * GS_NUM_COUNTERS, s) != hipSuccess)
+    return fail(GS_ERR_LAUNCH, "%s: memset failed", "gs_project_forward");
+  if (a->g.n == 0) return GS_OK;
+  if (!a->g.xyz || !a->g.color_logits || !a->g.opacity || !a->means2d || !a->conics || !a->radii ||
+      !a->vis || !a->records || !a->rects || !a->depth_keys)
+    return fail(GS_ERR_INVALID_ARG, "%s: null pointer", "gs_project_forward");
+  if (!a->g.cov3d && (!a->g.scaling || !a->g.rotation))
+    return fail(GS_ERR_INVALID_ARG, "%s: need cov3d or scaling+rotation", "gs_project_forward");
+  k_project_fwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  return check_launch("gs_project_forward");
+}
+
+size_t gs_radix_sort_workspace_bytes(int32_t n) {
+  const size_t nb = n > 0 ? div_up(n, kSortChunk) : 1;
+  return sizeof(uint32_t) * (kRadix * nb + kRadix) + 256;
+}
+
+gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
+                              int32_t n, int32_t begin_bit, int32_t end_bit, int32_t vals_are_iota,
+                              void *workspace, size_t workspace_bytes, int32_t *result_in_alt,
+                              gs_stream_t stream) {
+  if (!result_in_alt) return fail(GS_ERR_INVALID_ARG, "%s: null result_in_alt", "gs_radix_sort_pairs");
+  if (begin_bit < 0 || end_bit > 32 || begin_bit >= end_bit || n < 0)
+    return fail(GS_ERR_INVALID_ARG, "%s: bad bit range / n", "gs_radix_sort_pairs");
+  const int passes = (end_bit - begin_bit + kRadixBits - 1) / kRadixBits;
+  *result_in_alt = passes & 1;
+  if (n == 0) return GS_OK;
+  if (!keys || !vals || !keys_alt || !vals_alt || !workspace ||
+      workspace_bytes < gs_radix_sort_workspace_bytes(n))
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer or workspace too small", "gs_radix_sort_pairs");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)div_up(n, kSortChunk);
+  uint32_t *counts = (uint32_t *)workspace;
+  uint32_t *digit_total = counts + (size_t)kRadix * nb;
+  uint32_t *kin = keys, *vin = vals, *kout = keys_alt, *vout = vals_alt;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = begin_bit + p * kRadixBits;
+    const int nbits = (end_bit - shift) < kRadixBits ? (end_bit - shift) : kRadixBits;
+    if (hipMemsetAsync(digit_total, 0, sizeof(uint32_t) * kRadix, s) != hipSuccess)
+      return fail(GS_ERR_LAUNCH, "%s: memset failed", "gs_radix_sort_pairs");
+    k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, digit_total, nb);
+    k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, digit_total, nb);
+    k_radix_scatter<<<nb, kBlock, 0, s>>>(kin, (p == 0 && vals_are_iota) ? nullptr : vin, kout, vout, n, shift,
+                                          nbits, counts, nb);
+    gs_status st = check_launch("gs_radix_sort_pairs");
+    if (st) return st;
+    uint32_t *tk = kin, *tv = vin;
+    kin = kout;
+    vin = vout;
+    kout = tk;
+    vout = tv;
+  }
+  return GS_OK;
+}
+
+size_t gs_bin_workspace_bytes(int32_t n) {
+  return sizeof(uint32_t) * (size_t)(n > 0 ? div_up(n, kBinChunk) : 1) + 256;
+}
+
+gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
+  if (!a || !a->counters) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_bin_count");
+  if (a->n <= 0) return GS_OK;
+  if (!a->sorted_ids || !a->rects || !a->workspace || a->workspace_bytes < gs_bin_workspace_bytes(a->n))
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer or workspace too small", "gs_bin_count");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)div_up(a->n, kBinChunk);
+  uint32_t *partials = (uint32_t *)a->workspace;
+  k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials);
+  k_bin_scan_partials<<<1, kBlock, 0, s>>>(partials, nb, a->counters);
+  return check_launch("gs_bin_count");
+}
+
+gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream) {
+  if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_bin_emit");
+  if (a->n <= 0) return GS_OK;
+  if (!a->sorted_ids || !a->rects || !a->workspace || !a->tile_keys || !a->pair_gauss || !a->pair_offset)
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_bin_emit");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)div_up(a->n, kBinChunk);
+  k_bin_emit<<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace);
+  return check_launch("gs_bin_emit");
+}
+
+gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream) {
+  if (!a || !a->ranges) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_tile_ranges");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(a->ranges, 0, sizeof(uint32_t) * 2 * (size_t)a->num_tiles, s) != hipSuccess)
+    return fail(GS_ERR_LAUNCH, "%s: memset failed", "gs_tile_ranges");
+  if (a->num_pairs <= 0) return GS_OK;
+  if (!a->sorted_keys || !a->sorted_pairs || !a->pair_gauss || !a->sorted_gauss)
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_ranges");
+  k_tile_ranges<<<div_up(a->num_pairs, kBlock), kBlock, 0, s>>>(*a);
+  return check_launch("gs_tile_ranges");
+}
+
+gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
+  if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_forward");
+  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16", "gs_blend_forward");
+  if (a->tiles_x != (int)div_up(a->cam.image_width, GS_TILE) || a->tiles_y != (int)div_up(a->cam.image_height, GS_TILE))
+    return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_forward");
+  if (!a->ranges || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_acc || !a->pix_state)
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_forward");
+  hipStream_t s = (hipStream_t)stream;
+  k_blend_fwd<<<a->tiles_x * a->tiles_y, kBlock, 0, s>>>(*a);
+  return check_launch("gs_blend_forward");
+}
+
+gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
+  if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_backward");
+  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16", "gs_blend_backward");
+  if (a->tiles_x != (int)div_up(a->cam.image_width, GS_TILE) || a->tiles_y != (int)div_up(a->cam.image_height, GS_TILE))
+    return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_backward");
+  if (!a->ranges || !a->records || !a->pix_acc || !a->pix_state || !a->g_image || !a->pair_grads)
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_backward");
+  hipStream_t s = (hipStream_t)stream;
+  k_blend_bwd<<<a->tiles_x * a->tiles_y, kBlock, 0, s>>>(*a);
+  return check_launch("gs_blend_backward");
+}
+
+gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) {
+  if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_project_backward");
+  if (a->g.n <= 0) return GS_OK;
+  const bool raw = a->g.cov3d == nullptr;
+  if (!a->g.xyz || !a->g.color_logits || !a->means2d || !a->conics || !a->vis || !a->rects ||
+      !a->pair_offset || !a->d_xyz || !a->d_color_logits || !a->d_opacity ||
+      (raw ? (!a->g.scaling || !a->g.rotation || !a->d_scaling || !a->d_rotation) : !a->d_cov3d))
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_project_backward");
+  hipStream_t s = (hipStream_t)stream;
+  k_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  return check_launch("gs_project_backward");
+}
+
+}  // extern "C"

@@ -1,0 +1,263 @@
+"""Device pipeline + autograd for the render path.
+
+One `render` = the reference's four stages (renderer.py:31-114):
+  gs_project_forward   _project_gaussians_3d_to_2d + _frustum_culling
+  gs_radix_sort_pairs  _sort_gaussians_by_depth (32-bit depth keys)
+  gs_bin_count/emit    tile binning in depth order  (_tile_rasterization :263-298)
+  gs_radix_sort_pairs  stable sort of the entries by tile id
+  gs_tile_ranges       per-tile lists
+  gs_blend_forward     per-pixel compositing        (:273-367)
+and the backward: gs_blend_backward + gs_project_backward.
+
+All buffers are torch tensors from the caching allocator; the HIP library
+never allocates.  One host synchronisation per forward reads the visible
+count M and the tile-touch count T (needed to size the entry buffers, and
+for the reference's `vis_mask.sum() == 0` early return, renderer.py:74-83).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from . import _native as N
+
+
+@dataclass
+class CameraParams:
+    """Host-side scalars of one view, as renderer.py:140-152 derives them."""
+    image_width: int
+    image_height: int
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+    view: Tuple[float, ...]  # 12 floats, rows 0..2 of the W2C matrix
+    bg: Tuple[float, float, float]
+    radius_min: float = 0.01
+    radius_max: float = 50.0
+
+    @property
+    def tiles_x(self) -> int:
+        return (self.image_width + N.GS_TILE - 1) // N.GS_TILE
+
+    @property
+    def tiles_y(self) -> int:
+        return (self.image_height + N.GS_TILE - 1) // N.GS_TILE
+
+    def to_struct(self) -> N.GsCamera:
+        c = N.GsCamera()
+        c.image_width, c.image_height = int(self.image_width), int(self.image_height)
+        c.fx, c.fy, c.cx, c.cy = self.fx, self.fy, self.cx, self.cy
+        c.view = (C.c_float * 12)(*self.view)
+        c.radius_min, c.radius_max = self.radius_min, self.radius_max
+        c.bg = (C.c_float * 3)(*self.bg)
+        c.tile_size = N.GS_TILE
+        return c
+
+
+def _rows(t: torch.Tensor, cols: int) -> Tuple[torch.Tensor, int]:
+    """(tensor, row stride in floats) without copying when rows are dense."""
+    if t.dim() == 1 and cols == 1:
+        return t, t.stride(0)
+    if t.stride(-1) != 1 or t.shape[-1] != cols:
+        t = t.contiguous()
+    return t, t.stride(0)
+
+
+def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity) -> N.GsGaussians:
+    g = N.GsGaussians()
+    g.n = n
+    g.xyz, g.xyz_stride = N.ptr(xyz), xyz.stride(0)
+    g.cov3d = N.ptr(cov3d)
+    g.scaling, g.rotation = N.ptr(scaling), N.ptr(rotation)
+    g.color_logits, g.color_stride = N.ptr(logits), logits.stride(0)
+    g.opacity, g.opacity_stride = N.ptr(opacity), opacity.stride(0)
+    return g
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check_inputs(xyz: torch.Tensor):
+    if not xyz.is_cuda:
+        raise RuntimeError("the MI355X renderer needs Gaussians on a HIP device (got %s); "
+                           "there is no CPU path" % xyz.device)
+
+
+class _Frame:
+    """Intermediate device buffers of one forward, kept for the backward."""
+    __slots__ = ("records", "rects", "vis", "pair_offset", "ranges", "sorted_gauss", "sorted_pairs",
+                 "pix_acc", "pix_state", "M", "T")
+
+
+def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity):
+    lib = N.load()
+    dev = xyz.device
+    n = int(xyz.shape[0])
+    H, W = int(cam.image_height), int(cam.image_width)
+    f32, i32 = torch.float32, torch.int32
+    s = _stream()
+    cs = cam.to_struct()
+    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity)
+
+    means2d = torch.empty((n, 2), dtype=f32, device=dev)
+    conics = torch.empty((n, 2, 2), dtype=f32, device=dev)
+    radii = torch.empty((n,), dtype=f32, device=dev)
+    vis = torch.empty((n,), dtype=torch.bool, device=dev)
+    records = torch.empty((n, N.GS_RECORD_FLOATS), dtype=f32, device=dev)
+    rects = torch.empty((n, 2), dtype=i32, device=dev)
+    keys = torch.empty((2, n), dtype=i32, device=dev)
+    vals = torch.empty((2, n), dtype=i32, device=dev)
+    counters = torch.empty((N.GS_NUM_COUNTERS,), dtype=i32, device=dev)
+
+    pa = N.GsProjectArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(radii), N.ptr(vis), N.ptr(records),
+                         N.ptr(rects), N.ptr(keys[0]), N.ptr(counters))
+    N.check(lib.gs_project_forward(C.byref(pa), s), "gs_project_forward")
+
+    fr = _Frame()
+    fr.records, fr.rects, fr.vis = records, rects, vis
+    if n > 0:
+        ws = torch.empty((lib.gs_radix_sort_workspace_bytes(n),), dtype=torch.uint8, device=dev)
+        alt = C.c_int32(0)
+        N.check(lib.gs_radix_sort_pairs(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n, 0, 32, 1,
+                                        N.ptr(ws), ws.numel(), C.byref(alt), s), "depth sort")
+        sorted_ids = vals[alt.value]
+        bws = torch.empty((lib.gs_bin_workspace_bytes(n),), dtype=torch.uint8, device=dev)
+        ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(counters),
+                         N.ptr(bws), bws.numel(), 0, 0, 0)
+        N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
+        M, T = (int(v) for v in counters[:2].tolist())  # the one host sync
+    else:
+        M, T = 0, 0
+    fr.M, fr.T = M, T
+
+    if M == 0:
+        # renderer.py:74-83: bg once (not doubled, not clamped), zero alpha/depth
+        bg = torch.tensor(cam.bg, dtype=f32, device=dev).view(3, 1, 1)
+        image = bg.repeat(1, H, W)
+        alpha = torch.zeros((1, H, W), dtype=f32, device=dev)
+        depth = torch.zeros((1, H, W), dtype=f32, device=dev)
+        fr.pair_offset = torch.zeros((max(n, 1),), dtype=i32, device=dev)
+        return image, alpha, depth, means2d, conics, radii, vis, fr
+
+    num_tiles = cam.tiles_x * cam.tiles_y
+    tk = torch.empty((2, T), dtype=i32, device=dev)
+    tv = torch.empty((2, T), dtype=i32, device=dev)
+    pair_gauss = torch.empty((T,), dtype=i32, device=dev)
+    pair_offset = torch.empty((n,), dtype=i32, device=dev)
+    ba.tile_keys, ba.pair_gauss, ba.pair_offset = N.ptr(tk[0]), N.ptr(pair_gauss), N.ptr(pair_offset)
+    N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
+
+    bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
+    tws = torch.empty((lib.gs_radix_sort_workspace_bytes(T),), dtype=torch.uint8, device=dev)
+    alt = C.c_int32(0)
+    N.check(lib.gs_radix_sort_pairs(N.ptr(tk[0]), N.ptr(tv[0]), N.ptr(tk[1]), N.ptr(tv[1]), T, 0, bits, 1,
+                                    N.ptr(tws), tws.numel(), C.byref(alt), s), "tile sort")
+    sorted_keys, sorted_pairs = tk[alt.value], tv[alt.value]
+    ranges = torch.empty((num_tiles, 2), dtype=i32, device=dev)
+    sorted_gauss = torch.empty((T,), dtype=i32, device=dev)
+    ra = N.GsRangeArgs(T, num_tiles, N.ptr(sorted_keys), N.ptr(sorted_pairs), N.ptr(pair_gauss), N.ptr(ranges),
+                       N.ptr(sorted_gauss))
+    N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
+
+    image = torch.empty((3, H, W), dtype=f32, device=dev)
+    alpha = torch.empty((1, H, W), dtype=f32, device=dev)
+    depth = torch.empty((1, H, W), dtype=f32, device=dev)
+    pix_acc = torch.empty((H * W, 4), dtype=f32, device=dev)
+    pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
+    fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), N.ptr(sorted_gauss), N.ptr(records),
+                          N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state))
+    N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
+
+    fr.pair_offset, fr.ranges, fr.sorted_gauss, fr.sorted_pairs = pair_offset, ranges, sorted_gauss, sorted_pairs
+    fr.pix_acc, fr.pix_state = pix_acc, pix_state
+    return image, alpha, depth, means2d, conics, radii, vis, fr
+
+
+def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotation, logits, opacity,
+                      means2d, conics, g_image, g_alpha, g_depth, g_means2d, g_conics):
+    lib = N.load()
+    dev = xyz.device
+    n = int(xyz.shape[0])
+    f32 = torch.float32
+    s = _stream()
+    cs = cam.to_struct()
+    pair_grads = None
+    pixel_grads = g_image is not None or g_alpha is not None or g_depth is not None
+    if fr.M > 0 and fr.T > 0 and pixel_grads:
+        if g_image is None:
+            g_image = torch.zeros((3, cam.image_height, cam.image_width), dtype=f32, device=dev)
+        g_image = g_image.contiguous()
+        g_alpha = None if g_alpha is None else g_alpha.contiguous()
+        g_depth = None if g_depth is None else g_depth.contiguous()
+        pair_grads = torch.empty((max(fr.T, 1), N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
+        ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
+                              N.ptr(fr.sorted_pairs), N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
+                              N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(pair_grads))
+        N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
+    raw = cov3d is None
+    d_xyz = torch.empty((n, 3), dtype=f32, device=dev)
+    d_cov = None if raw else torch.empty((n, 3, 3), dtype=f32, device=dev)
+    d_scl = torch.empty((n, 3), dtype=f32, device=dev) if raw else None
+    d_rot = torch.empty((n, 4), dtype=f32, device=dev) if raw else None
+    d_col = torch.empty((n, 3), dtype=f32, device=dev)
+    d_op = torch.empty((n,), dtype=f32, device=dev)
+    gm = None if g_means2d is None else g_means2d.contiguous()
+    gc = None if g_conics is None else g_conics.contiguous()
+    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity)
+    pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
+                            N.ptr(fr.pair_offset), N.ptr(pair_grads), N.ptr(gm), N.ptr(gc), N.ptr(d_xyz),
+                            N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op))
+    N.check(lib.gs_project_backward(C.byref(pb), s), "gs_project_backward")
+    return d_xyz, d_cov, d_scl, d_rot, d_col, d_op
+
+
+class RasterizeGaussians(torch.autograd.Function):
+    """Differentiable render: inputs are the model accessors' tensors, outputs
+    are (image, alpha, depth, viewspace_points, conics, radii, visibility)."""
+
+    @staticmethod
+    def forward(ctx, xyz, cov3d, scaling, rotation, logits, opacity, cam: CameraParams):
+        image, alpha, depth, means2d, conics, radii, vis, fr = forward_pipeline(
+            cam, xyz, cov3d, scaling, rotation, logits, opacity)
+        ctx.cam, ctx.frame = cam, fr
+        ctx.save_for_backward(xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics)
+        ctx.mark_non_differentiable(radii, vis)
+        ctx.set_materialize_grads(False)
+        return image, alpha, depth, means2d, conics, radii, vis
+
+    @staticmethod
+    def backward(ctx, g_image, g_alpha, g_depth, g_means2d, g_conics, _g_radii, _g_vis):
+        xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics = ctx.saved_tensors
+        g_conics = None if g_conics is None else g_conics.reshape(-1, 4)
+        d_xyz, d_cov, d_scl, d_rot, d_col, d_op = backward_pipeline(
+            ctx.cam, ctx.frame, xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics,
+            g_image, None if g_alpha is None else g_alpha, g_depth, g_means2d, g_conics)
+        need = ctx.needs_input_grad
+        return (d_xyz if need[0] else None,
+                d_cov if (cov3d is not None and need[1]) else None,
+                d_scl if (scaling is not None and need[2]) else None,
+                d_rot if (rotation is not None and need[3]) else None,
+                d_col if need[4] else None,
+                d_op.view(opacity.shape) if need[5] else None,
+                None)
+
+
+def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity):
+    _check_inputs(xyz)
+    if cov3d is not None:
+        cov3d = cov3d.reshape(-1, 3, 3)
+        if not cov3d.is_contiguous():
+            cov3d = cov3d.contiguous()
+    else:
+        scaling = scaling.contiguous()
+        rotation = rotation.contiguous()
+    xyz, _ = _rows(xyz, 3)
+    logits, _ = _rows(logits, 3)
+    opacity, _ = _rows(opacity, 1)
+    return RasterizeGaussians.apply(xyz, cov3d, scaling, rotation, logits, opacity, cam)

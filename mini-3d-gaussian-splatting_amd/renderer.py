@@ -1,0 +1,101 @@
+"""Drop-in GaussianRenderer / RenderSettings (reference: src/core/renderer.py).
+
+Same class names, constructor arguments, render() signature and output
+dict as the reference (renderer.py:13-114).  The four stages run as HIP
+kernels (see rasterizer.py); the duck-typed inputs are read exactly where
+the reference reads them:
+
+  camera._width/_height/_FoVx/_FoVy, camera.world_view_transform()  (:140-150)
+  gaussians.get_xyz (:135), get_covariance (:166), get_features or
+  _features_dc (:88-92), get_opacity (:94)
+
+Differences a caller can observe (all documented in DESIGN.md):
+  * `world_view_transform` may be a method (what the reference calls) or a
+    tensor/property (what the reference's own Camera defines).
+  * When `gaussians` is this package's GaussianModel, covariance is built
+    inside the projection kernel from the raw `_scaling`/`_rotation` (same
+    math as GaussianModel.compute_3d_covariance) and colours are read from
+    `_features_dc` instead of materialising get_features; gradients reach the
+    same leaves, except `_features_rest`, whose gradient is identically zero
+    in the reference and is left as None here.
+  * `radii` and `visibility_filter` carry no gradient.
+  * `settings.scale_modifier` and `settings.debug` are ignored, as in the
+    reference.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict
+
+import torch
+
+from .rasterizer import CameraParams, rasterize
+
+
+@dataclass
+class RenderSettings:
+    """renderer.py:13-20"""
+    image_height: int
+    image_width: int
+    bg_color: torch.Tensor
+    scale_modifier: float = 1.0
+    debug: bool = False
+
+
+def _world_view(camera) -> torch.Tensor:
+    wv = camera.world_view_transform
+    if callable(wv):
+        wv = wv()
+    return torch.as_tensor(wv)
+
+
+def camera_params(camera, settings: RenderSettings, radius_min=0.01, radius_max=50.0) -> CameraParams:
+    """Host scalars of renderer.py:140-152 (python double -> fp32 in the ABI)."""
+    W, H = camera._width, camera._height
+    fx = 0.5 * W / math.tan(camera._FoVx * 0.5)
+    fy = 0.5 * H / math.tan(camera._FoVy * 0.5)
+    wv = _world_view(camera).detach().to("cpu", torch.float32).reshape(4, 4)
+    view = tuple(float(v) for v in wv[:3, :].reshape(-1).tolist())
+    bg = settings.bg_color
+    bg = tuple(float(v) for v in torch.as_tensor(bg).detach().to("cpu", torch.float32).reshape(3).tolist())
+    return CameraParams(int(settings.image_width), int(settings.image_height), fx, fy, W * 0.5, H * 0.5,
+                        view, bg, float(radius_min), float(radius_max))
+
+
+class GaussianRenderer:
+    """renderer.py:22-114"""
+
+    def __init__(self, tile_size=16, radius_min=0.01, radius_max=50.0):
+        if tile_size != 16:
+            raise ValueError("the MI355X rasterizer implements tile_size=16 (the reference default)")
+        self.tile_size = tile_size
+        self.radius_min = radius_min
+        self.radius_max = radius_max
+        self.device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+    def render(self, camera, gaussians, settings: RenderSettings) -> Dict[str, torch.Tensor]:
+        cam = camera_params(camera, settings, self.radius_min, self.radius_max)
+        xyz = gaussians.get_xyz
+        if getattr(gaussians, "_gs_fused_covariance", False):
+            cov3d, scaling, rotation = None, gaussians._scaling, gaussians._rotation
+            logits = gaussians._features_dc[:, 0, :]
+        else:
+            cov3d, scaling, rotation = gaussians.get_covariance, None, None
+            feats = gaussians.get_features
+            if feats.dim() == 3 and feats.shape[1] >= 1:
+                logits = feats[:, 0, :]
+            else:
+                logits = gaussians._features_dc.squeeze(1)
+        opacity = gaussians.get_opacity.squeeze(1)
+        image, alpha, depth, means2d, conics, radii, vis = rasterize(
+            cam, xyz, cov3d, scaling, rotation, logits, opacity)
+        return {
+            "image": image,
+            "alpha": alpha,
+            "depth": depth,
+            "viewspace_points": means2d,
+            "visibility_filter": vis,
+            "radii": radii,
+            "conics": conics,
+        }

@@ -1,0 +1,188 @@
+"""GPU parity: the HIP render path (through the C ABI) against the
+reference's golden vectors and the pinned CPU oracle.
+
+Tolerances are in tests/golden_io.py (1e-4 abs on image/alpha, gated depth,
+grads 2e-3 x max|ref| + 1e-5)."""
+import numpy as np
+import pytest
+import torch
+
+import golden_io as G
+from stubs import Cam, Gauss, grad_or_zero
+
+pytestmark = pytest.mark.gpu
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy()
+
+
+def _outputs(out):
+    return dict(image=_np(out["image"]), alpha=_np(out["alpha"]), depth=_np(out["depth"]),
+                means2d=_np(out["viewspace_points"]), conics=_np(out["conics"]), radii=_np(out["radii"]),
+                vis=_np(out["visibility_filter"]).astype(bool))
+
+
+def _render_stub(pkg, dev, f, method=True):
+    cam = Cam(f["cam_width"], f["cam_height"], f["fovx"], f["fovy"], f["wv"], method=method)
+    st = pkg.RenderSettings(image_height=int(f["height"]), image_width=int(f["width"]),
+                            bg_color=torch.tensor(np.asarray(f["bg"], np.float32)))
+    g = Gauss(f["xyz"], f["cov3d"], f["color_logits"], f["opacity"], dev)
+    return g, pkg.GaussianRenderer().render(cam, g, st)
+
+
+def _loss(out, f, dev):
+    t = lambda k: torch.tensor(np.asarray(f[k], np.float32), device=dev)
+    L = (out["image"] * t("g_image")).sum() + (out["alpha"] * t("g_alpha")).sum() + (out["depth"] * t("g_depth")).sum()
+    if "g_means2d" in f:
+        L = L + (out["viewspace_points"] * t("g_means2d")).sum() + (out["conics"] * t("g_conics")).sum()
+    return L
+
+
+STUB_CASES = [n for n in G.fixture_names() if "scaling" not in G.load(n)]
+
+
+@pytest.mark.parametrize("name", STUB_CASES)
+def test_reference_fixture(pkg, cuda, name):
+    f = G.load(name)
+    g, out = _render_stub(pkg, cuda, f)
+    o = _outputs(out)
+    errs = G.check_image(o, f) + G.check_projection(o, f)
+    assert out["image"].shape == (3, int(f["height"]), int(f["width"]))
+    assert out["visibility_filter"].dtype == torch.bool
+    if "g_image" in f:
+        _loss(out, f, cuda).backward()
+        n = f["xyz"].shape[0]
+        errs += G.check_grad("xyz", grad_or_zero(g.xyz, (n, 3)), f["d_xyz"])
+        errs += G.check_grad("cov3d", grad_or_zero(g.cov, (n, 3, 3)), f["d_cov3d"])
+        errs += G.check_grad("color", grad_or_zero(g.feats, (n, 16, 3))[:, 0], f["d_color_logits"])
+        errs += G.check_grad("opacity", grad_or_zero(g.op, (n, 1))[:, 0], f["d_opacity"])
+        rest = grad_or_zero(g.feats, (n, 16, 3))[:, 1:]
+        assert not rest.any(), "features_rest must get a zero gradient (reference only renders DC)"
+    assert not errs, errs
+
+
+def test_reference_model_path(pkg, cuda):
+    """Raw-parameter (fused covariance) path vs reference GaussianModel grads."""
+    f = G.load("model_random")
+    m = pkg.GaussianModel()
+    n = f["xyz"].shape[0]
+    T = lambda a, shape=None: torch.tensor(np.asarray(a, np.float32)).reshape(shape or np.shape(a)).to(cuda)
+    m._set(T(f["xyz"]), T(f["color_logits"], (n, 1, 3)), torch.zeros(n, 15, 3, device=cuda), T(f["scaling"]),
+           T(f["rotation"]), T(f["opacity_raw"], (n, 1)))
+    cam = Cam(f["cam_width"], f["cam_height"], f["fovx"], f["fovy"], f["wv"])
+    st = pkg.RenderSettings(image_height=int(f["height"]), image_width=int(f["width"]),
+                            bg_color=torch.tensor(np.asarray(f["bg"], np.float32)))
+    out = pkg.GaussianRenderer().render(cam, m, st)
+    o = _outputs(out)
+    errs = G.check_image(o, f) + G.check_projection(o, f)
+    _loss(out, f, cuda).backward()
+    errs += G.check_grad("xyz", _np(m._xyz.grad), f["d_xyz"])
+    errs += G.check_grad("scaling", _np(m._scaling.grad), f["d_scaling"])
+    errs += G.check_grad("rotation", _np(m._rotation.grad), f["d_rotation"])
+    errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], f["d_color_logits"])
+    errs += G.check_grad("opacity", _np(m._opacity.grad)[:, 0], f["d_opacity_raw"])
+    assert not errs, errs
+
+
+def test_tensor_world_view_transform(pkg, cuda):
+    """world_view_transform as a tensor attribute (reference Camera style)."""
+    f = G.load("posed_camera")
+    _, out = _render_stub(pkg, cuda, f, method=False)
+    assert not G.check_image(_outputs(out), f)
+
+
+def test_kat_front_to_back(pkg, cuda):
+    """test_renderer.py:127-161 restated: alpha 0.75, rgb 0.5 s(c0)+0.25 s(c1), depth 4/3."""
+    cam = Cam(64, 64, np.radians(60), np.radians(60))
+    st = pkg.RenderSettings(64, 64, torch.zeros(3))
+    g = Gauss([[0, 0, 1], [0, 0, 2]], np.stack([np.diag([1e-4] * 3)] * 2), [[1, 0, 0], [0, 1, 0]], [0.5, 0.5], cuda)
+    out = pkg.GaussianRenderer().render(cam, g, st)
+    s = torch.sigmoid
+    exp = 0.5 * s(torch.tensor([1.0, 0, 0])) + 0.25 * s(torch.tensor([0.0, 1, 0]))
+    assert abs(out["alpha"][0, 32, 32].item() - 0.75) < 1e-3
+    assert torch.allclose(out["image"][:, 32, 32].cpu(), exp, atol=1e-3)
+    assert abs(out["depth"][0, 32, 32].item() - 4 / 3) < 2e-2
+
+
+def test_all_culled_returns_bg(pkg, cuda):
+    """test_renderer.py:113-125: everything behind the camera -> image == bg, alpha 0."""
+    cam = Cam(32, 32, np.radians(60), np.radians(60))
+    st = pkg.RenderSettings(64, 64, torch.tensor([0.2, 0.3, 0.4]))
+    g = Gauss([[0, 0, -1], [0, 0, -2]], np.stack([np.diag([1e-4] * 3)] * 2), [[1, 0, 0], [0, 1, 0]], [0.5, 0.5], cuda)
+    out = pkg.GaussianRenderer().render(cam, g, st)
+    assert torch.allclose(out["image"].cpu(), torch.tensor([0.2, 0.3, 0.4]).view(3, 1, 1).expand(3, 64, 64))
+    assert torch.count_nonzero(out["alpha"]) == 0
+    out["viewspace_points"].sum().backward()  # cotangent on means2D still flows
+    assert g.xyz.grad is not None and torch.isfinite(g.xyz.grad).all()
+
+
+def _oracle_scene(sc, cov, bg):
+    o = G.oracle()
+    return o.Scene(xyz=sc.xyz.numpy(), cov3d=cov, color_logits=sc.features_dc[:, 0].numpy(),
+                   opacity=torch.sigmoid(sc.opacity[:, 0]).numpy(), wv=np.eye(4), width=sc.width,
+                   height=sc.height, fovx=sc.fovx, fovy=sc.fovy, bg=np.asarray(bg, np.float32))
+
+
+@pytest.mark.parametrize("n,w,h,sig", [(3000, 200, 152, (0.01, 0.05)), (20000, 320, 240, (0.002, 0.02))])
+def test_random_scene_vs_oracle(pkg, cuda, n, w, h, sig):
+    """Larger random scenes (partial edge tiles, many overlaps) vs the oracle."""
+    syn = pkg.synthetic
+    sc = syn.make_scene(n, w, h, seed=n, sigma_range=sig)
+    m = syn.to_model(sc, pkg.GaussianModel, cuda)
+    cov = G.oracle().covariance(sc.scaling.numpy(), sc.rotation.numpy())
+    bg = [0.1, 0.0, 0.3]
+    cam = Cam(w, h, sc.fovx, sc.fovy)
+    out = pkg.GaussianRenderer().render(cam, m, pkg.RenderSettings(h, w, torch.tensor(bg)))
+    rng = np.random.default_rng(1)
+    gi, ga, gd = (rng.uniform(-1, 1, s).astype(np.float32) for s in ((3, h, w), (1, h, w), (1, h, w)))
+    L = sum((out[k] * torch.tensor(v, device=cuda)).sum() for k, v in (("image", gi), ("alpha", ga), ("depth", gd)))
+    L.backward()
+    ref = G.oracle().render_backward(_oracle_scene(sc, cov, bg), gi, ga, gd)
+    errs = G.check_image(_outputs(out), ref) + G.check_projection(_outputs(out), ref)
+    ds, dr = G.oracle().covariance_backward(sc.scaling.numpy(), sc.rotation.numpy(), ref["grads"]["cov3d"])
+    op = torch.sigmoid(sc.opacity[:, 0]).numpy()
+    errs += G.check_grad("xyz", _np(m._xyz.grad), ref["grads"]["xyz"])
+    errs += G.check_grad("scaling", _np(m._scaling.grad), ds)
+    errs += G.check_grad("rotation", _np(m._rotation.grad), dr)
+    errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"])
+    errs += G.check_grad("opacity", _np(m._opacity.grad)[:, 0], ref["grads"]["opacity"] * op * (1 - op))
+    assert not errs, errs
+
+
+def test_radix_sort_matches_stable_argsort(pkg, cuda):
+    import ctypes as C
+    N = pkg._native
+    lib = N.load()
+    rng = np.random.default_rng(3)
+    for n, bits in ((1, 8), (1000, 13), (123457, 32), (70000, 4)):
+        k = rng.integers(0, 1 << min(bits, 31), n, dtype=np.int64).astype(np.uint32)
+        if bits == 32:
+            k[::7] = 0xFFFFFFFF
+        keys = torch.tensor(k.view(np.int32), device=cuda)
+        kk = torch.empty((2, n), dtype=torch.int32, device=cuda)
+        vv = torch.empty((2, n), dtype=torch.int32, device=cuda)
+        kk[0].copy_(keys)
+        ws = torch.empty(lib.gs_radix_sort_workspace_bytes(n), dtype=torch.uint8, device=cuda)
+        alt = C.c_int32(0)
+        N.check(lib.gs_radix_sort_pairs(N.ptr(kk[0]), N.ptr(vv[0]), N.ptr(kk[1]), N.ptr(vv[1]), n, 0, bits, 1,
+                                        N.ptr(ws), ws.numel(), C.byref(alt), torch.cuda.current_stream().cuda_stream),
+                "sort")
+        order = np.argsort(k, kind="stable")
+        assert np.array_equal(vv[alt.value].cpu().numpy().view(np.uint32), order.astype(np.uint32))
+        assert np.array_equal(kk[alt.value].cpu().numpy().view(np.uint32), k[order])
+
+
+def test_deterministic(pkg, cuda):
+    """No float atomics anywhere: two runs are bit-identical, grads included."""
+    syn = pkg.synthetic
+    sc = syn.make_scene(50000, 480, 270, seed=5, sigma_range=(0.002, 0.02))
+    res = []
+    for _ in range(2):
+        m = syn.to_model(sc, pkg.GaussianModel, cuda)
+        out = pkg.GaussianRenderer().render(Cam(480, 270, sc.fovx, sc.fovy), m,
+                                            pkg.RenderSettings(270, 480, torch.zeros(3)))
+        out["image"].sum().backward()
+        res.append((out["image"].clone(), m._xyz.grad.clone(), m._rotation.grad.clone()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
