@@ -1,0 +1,237 @@
+"""Benchmark: rendered Mpix/s, fwd+bwd, 1M Gaussians at 1920x1080 (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (driver, N > 1)
+
+One step on each rank = one training step of one view: zero_grad ->
+GaussianRenderer.render -> backward of a fixed random cotangent on
+(image, alpha, depth) -> [N>1] RCCL all-reduce (mean) of the Gaussian
+gradients -> Adam step.  Rank r renders view r of the same replicated 1M
+Gaussian model (weak scaling: one 1080p view per GPU per step).  Inputs are
+resident in HBM before the timed region.  `value` = all ranks' pixels /
+max-over-ranks step time.
+
+Also reported: the roofline of the dominant kernel (HIP events on the
+kernels' own stream, averaged over the timed steps) and a CPU baseline (the
+oracle, a C restatement of the reference path, on the host cores, rank 0,
+N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "rendered Mpix/s fwd+bwd @1080p, 1M Gaussians; PSNR vs ref; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TFLOPS = 157.3     # FP32 vector, spec (FMA = 2)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gaussians", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--no-optimizer", action="store_true", help="time render fwd+bwd only")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def view_matrix(rank: int) -> torch.Tensor:
+    """Rank r's camera: a small yaw/translation of the identity view (all
+    views look at the same synthetic volume)."""
+    if rank == 0:
+        return torch.eye(4)
+    ang = 0.02 * rank * (1 if rank % 2 else -1)
+    c, s = math.cos(ang), math.sin(ang)
+    wv = torch.eye(4)
+    wv[:3, :3] = torch.tensor([[c, 0.0, s], [0.0, 1.0, 0.0], [-s, 0.0, c]])
+    wv[:3, 3] = torch.tensor([0.01 * rank, 0.0, 0.0])
+    return wv
+
+
+class BenchCamera:
+    def __init__(self, w, h, fovx, fovy, wv):
+        self._width, self._height, self._FoVx, self._FoVy, self._wv = w, h, fovx, fovy, wv
+
+    def world_view_transform(self):
+        return self._wv
+
+
+def algorithmic_counts(fr, H, W, tiles_x, tiles_y):
+    """R (records consumed per tile: list prefix up to the deepest pixel's
+    last evaluated entry), E (evaluated pairs), from the forward's saved
+    per-pixel state."""
+    neval = fr.pix_state[:, 1].contiguous().view(torch.int32).view(H, W).to(torch.int64)
+    E = int(neval.sum())
+    pad = torch.zeros(tiles_y * 16, tiles_x * 16, dtype=torch.int64, device=neval.device)
+    pad[:H, :W] = neval
+    per_tile = pad.view(tiles_y, 16, tiles_x, 16).amax(dim=(1, 3))
+    R = int(per_tile.sum())
+    return R, E
+
+
+def main():
+    a = parse()
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    from mini3dgs_amd.rasterizer import StageTimer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    W, H, n = a.width, a.height, a.gaussians
+    scene = pkg.synthetic.make_scene(n, W, H, seed=0)
+    model = pkg.synthetic.to_model(scene, pkg.GaussianModel, dev)
+    params = model.grad_parameters()
+    opt = None if a.no_optimizer else torch.optim.Adam(
+        [{"params": [model._xyz], "lr": 1.6e-4}, {"params": [model._features_dc], "lr": 2.5e-3},
+         {"params": [model._opacity], "lr": 0.05}, {"params": [model._scaling], "lr": 5e-3},
+         {"params": [model._rotation], "lr": 1e-3}], fused=True)
+    cam = BenchCamera(W, H, scene.fovx, scene.fovy, view_matrix(rank))
+    settings = pkg.RenderSettings(image_height=H, image_width=W, bg_color=torch.zeros(3))
+    renderer = pkg.GaussianRenderer()
+    g = torch.Generator().manual_seed(1)
+    cot = [(torch.rand(s, generator=g) * 2 - 1).to(dev) for s in ((3, H, W), (1, H, W), (1, H, W))]
+    reducer = pkg.distributed.GradAllReduce(params, dist) if dist is not None else None
+    frames = []
+
+    def step():
+        if opt is not None:
+            opt.zero_grad(set_to_none=True)
+        else:
+            for p in params:
+                p.grad = None
+        out = renderer.render(cam, model, settings)
+        torch.autograd.backward([out["image"], out["alpha"], out["depth"]], cot)
+        if reducer is not None:
+            reducer.all_reduce_mean()
+        if opt is not None:
+            opt.step()
+        frames.append(out)
+
+    # keep the model fixed for a reproducible workload: restore params after
+    # warmup (Adam moves them), then time K steps.
+    snapshot = [p.detach().clone() for p in params]
+    for _ in range(a.warmup):
+        step()
+        frames.clear()
+    with torch.no_grad():
+        for p, s0 in zip(params, snapshot):
+            p.copy_(s0)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    StageTimer.enabled = True
+    StageTimer.reset()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        frames = frames[-1:]
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    StageTimer.enabled = False
+    dt = t1 - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    stages = {k: sum(v) / len(v) for k, v in StageTimer.durations_ms().items()}
+    ms_per_step = 1000.0 * dt / a.steps
+    mpix = world * H * W * a.steps / dt / 1e6
+
+    if rank == 0:
+        # --- roofline of the dominant kernel -------------------------------
+        from mini3dgs_amd.rasterizer import forward_pipeline  # noqa: F401
+        tiles_x, tiles_y = (W + 15) // 16, (H + 15) // 16
+        with torch.no_grad():
+            out = renderer.render(cam, model, settings)
+        # re-run the forward pipeline to read its frame state (not timed)
+        from mini3dgs_amd import rasterizer as RZ
+        camp = pkg.camera_params(cam, settings)
+        _, _, _, _, _, _, _, fr = RZ.forward_pipeline(
+            camp, model._xyz, None, model._scaling, model._rotation, model._features_dc[:, 0, :],
+            torch.sigmoid(model._opacity).squeeze(1))
+        R, E = algorithmic_counts(fr, H, W, tiles_x, tiles_y)
+        M, T = fr.M, fr.T
+        num_tiles = tiles_x * tiles_y
+        # algorithmic bytes per launch
+        bytes_fwd = 44 * R + 8 * num_tiles + 20 * H * W + 24 * H * W
+        bytes_bwd = 44 * R + 4 * R + 40 * R + 8 * num_tiles + (24 + 20) * H * W
+        flops_fwd = 26 * E
+        kern = {"blend_fwd": (bytes_fwd, flops_fwd), "blend_bwd": (bytes_bwd, None)}
+        dom = max((k for k in kern if k in stages), key=lambda k: stages[k])
+        t_ms = stages[dom]
+        ach = kern[dom][0] / (t_ms * 1e-3) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_ms": round(t_ms, 4),
+                "algorithmic_bytes_per_launch": int(kern[dom][0])}
+        if kern[dom][1]:
+            tf = kern[dom][1] / (t_ms * 1e-3) / 1e12
+            roof["valu"] = {"achieved_tflops": round(tf, 2), "peak_tflops": VALU_PEAK_TFLOPS,
+                            "frac": round(tf / VALU_PEAK_TFLOPS, 4)}
+        # --- CPU baseline ---------------------------------------------------
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(scene, W, H, cot, a.cpu_threads)
+        line = {
+            "metric": METRIC, "value": round(mpix, 3), "unit": "Mpix/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "C3: 1M synthetic Gaussians (SURVEY 8d), 1920x1080, 16x16 tiles, "
+                                   "render fwd+bwd" + ("" if opt is None else " + grad all-reduce + Adam step"),
+                       "gaussians": n, "width": W, "height": H, "views_per_step": world,
+                       "parallelism": f"dp{world} (one view per GPU)", "visible": M, "tile_touches": T,
+                       "records_consumed": R, "evaluated_pairs": E},
+            "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(scene, W, H, cot, threads):
+    """Oracle (C restatement of the reference render path) fwd+bwd on the
+    host cores for the same C3 frame; bounded: one frame."""
+    import numpy as np
+    from oracle import oracle as orc  # CPU baseline leg: test infrastructure only
+    cov = orc.covariance(scene.scaling.numpy(), scene.rotation.numpy())
+    s = orc.Scene(xyz=scene.xyz.numpy(), cov3d=cov, color_logits=scene.features_dc[:, 0].numpy(),
+                  opacity=torch.sigmoid(scene.opacity[:, 0]).numpy(), wv=np.eye(4), width=W, height=H,
+                  fovx=scene.fovx, fovy=scene.fovy, bg=np.zeros(3, np.float32))
+    gi, ga, gd = (c.cpu().numpy() for c in cot)
+    t0 = time.perf_counter()
+    orc.render_backward(s, gi, ga, gd, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(H * W / dt / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"one full C3 frame ({W}x{H}, {scene.xyz.shape[0]} Gaussians) fwd+bwd, "
+                      f"oracle/gs_oracle.c with OpenMP x{threads}, {dt:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()

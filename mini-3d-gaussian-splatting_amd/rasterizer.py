@@ -83,6 +83,37 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+class StageTimer:
+    """Optional per-stage HIP-event timing on the stream the kernels are
+    launched on (torch's current stream).  Disabled unless a bench enables it;
+    when disabled, mark() is a no-op."""
+    enabled = False
+    events: list = []
+
+    @classmethod
+    def mark(cls, name: str):
+        if cls.enabled:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            cls.events.append((name, e))
+
+    @classmethod
+    def reset(cls):
+        cls.events = []
+
+    @classmethod
+    def durations_ms(cls):
+        """{stage: [ms per occurrence]} -- stage = interval from its mark to the next."""
+        torch.cuda.synchronize()
+        out = {}
+        ev = cls.events
+        for (name, e0), (_, e1) in zip(ev[:-1], ev[1:]):
+            if name.startswith("~"):
+                continue
+            out.setdefault(name, []).append(e0.elapsed_time(e1))
+        return out
+
+
 def _check_inputs(xyz: torch.Tensor):
     if not xyz.is_cuda:
         raise RuntimeError("the MI355X renderer needs Gaussians on a HIP device (got %s); "
@@ -115,6 +146,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     vals = torch.empty((2, n), dtype=i32, device=dev)
     counters = torch.empty((N.GS_NUM_COUNTERS,), dtype=i32, device=dev)
 
+    StageTimer.mark("project_fwd")
     pa = N.GsProjectArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(radii), N.ptr(vis), N.ptr(records),
                          N.ptr(rects), N.ptr(keys[0]), N.ptr(counters))
     N.check(lib.gs_project_forward(C.byref(pa), s), "gs_project_forward")
@@ -123,6 +155,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     fr.records, fr.rects, fr.vis = records, rects, vis
     if n > 0:
         ws = torch.empty((lib.gs_radix_sort_workspace_bytes(n),), dtype=torch.uint8, device=dev)
+        StageTimer.mark("depth_sort")
         alt = C.c_int32(0)
         N.check(lib.gs_radix_sort_pairs(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n, 0, 32, 1,
                                         N.ptr(ws), ws.numel(), C.byref(alt), s), "depth sort")
@@ -130,7 +163,9 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         bws = torch.empty((lib.gs_bin_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(counters),
                          N.ptr(bws), bws.numel(), 0, 0, 0)
+        StageTimer.mark("bin_count")
         N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
+        StageTimer.mark("~sync")
         M, T = (int(v) for v in counters[:2].tolist())  # the one host sync
     else:
         M, T = 0, 0
@@ -151,11 +186,13 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     pair_gauss = torch.empty((T,), dtype=i32, device=dev)
     pair_offset = torch.empty((n,), dtype=i32, device=dev)
     ba.tile_keys, ba.pair_gauss, ba.pair_offset = N.ptr(tk[0]), N.ptr(pair_gauss), N.ptr(pair_offset)
+    StageTimer.mark("bin_emit")
     N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
 
     bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
     tws = torch.empty((lib.gs_radix_sort_workspace_bytes(T),), dtype=torch.uint8, device=dev)
     alt = C.c_int32(0)
+    StageTimer.mark("tile_sort")
     N.check(lib.gs_radix_sort_pairs(N.ptr(tk[0]), N.ptr(tv[0]), N.ptr(tk[1]), N.ptr(tv[1]), T, 0, bits, 1,
                                     N.ptr(tws), tws.numel(), C.byref(alt), s), "tile sort")
     sorted_keys, sorted_pairs = tk[alt.value], tv[alt.value]
@@ -163,6 +200,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     sorted_gauss = torch.empty((T,), dtype=i32, device=dev)
     ra = N.GsRangeArgs(T, num_tiles, N.ptr(sorted_keys), N.ptr(sorted_pairs), N.ptr(pair_gauss), N.ptr(ranges),
                        N.ptr(sorted_gauss))
+    StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
     image = torch.empty((3, H, W), dtype=f32, device=dev)
@@ -172,7 +210,9 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
     fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), N.ptr(sorted_gauss), N.ptr(records),
                           N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state))
+    StageTimer.mark("blend_fwd")
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
+    StageTimer.mark("~end_fwd")
 
     fr.pair_offset, fr.ranges, fr.sorted_gauss, fr.sorted_pairs = pair_offset, ranges, sorted_gauss, sorted_pairs
     fr.pix_acc, fr.pix_state = pix_acc, pix_state
@@ -199,6 +239,7 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.sorted_pairs), N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(pair_grads))
+        StageTimer.mark("blend_bwd")
         N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
     raw = cov3d is None
     d_xyz = torch.empty((n, 3), dtype=f32, device=dev)
@@ -213,7 +254,9 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
                             N.ptr(fr.pair_offset), N.ptr(pair_grads), N.ptr(gm), N.ptr(gc), N.ptr(d_xyz),
                             N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op))
+    StageTimer.mark("project_bwd")
     N.check(lib.gs_project_backward(C.byref(pb), s), "gs_project_backward")
+    StageTimer.mark("~end_bwd")
     return d_xyz, d_cov, d_scl, d_rot, d_col, d_op
 
 
