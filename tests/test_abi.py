@@ -1,0 +1,71 @@
+"""The C-ABI library loads and exports every symbol include/gsplat_mi355x.h
+declares; struct layouts of the ctypes mirror equal the C compiler's; entry
+points reject bad arguments with a status + message (no GPU needed: these
+return before any HIP call)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "gsplat_mi355x.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:gs_status|size_t|int32_t|const char \*)\s*(gs_\w+)\s*\(", src, re.M)))
+
+
+def test_header_and_binding_agree(pkg):
+    assert declared_functions() == sorted(pkg._native.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib = pkg._native.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", pkg._native.LIB_PATH], capture_output=True, text=True).stdout
+    for name in declared_functions():
+        assert re.search(r"\bT %s$" % name, out, re.M), name
+
+
+def test_abi_version(pkg):
+    assert pkg._native.load().gs_abi_version() == pkg._native.GS_ABI_VERSION
+
+
+def test_struct_layouts_match_c(pkg, tmp_path):
+    N = pkg._native
+    names = ["gs_camera", "gs_gaussians", "gs_project_args", "gs_bin_args", "gs_range_args",
+             "gs_blend_fwd_args", "gs_blend_bwd_args", "gs_project_bwd_args"]
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "gsplat_mi355x.h"\nint main(){' +
+                   "".join('printf("%%zu\\n", sizeof(%s));' % n for n in names) + "}")
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    sizes = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    py = [C.sizeof(t) for t in (N.GsCamera, N.GsGaussians, N.GsProjectArgs, N.GsBinArgs, N.GsRangeArgs,
+                                N.GsBlendFwdArgs, N.GsBlendBwdArgs, N.GsProjectBwdArgs)]
+    assert sizes == py
+
+
+def test_bad_arguments_are_reported(pkg):
+    N = pkg._native
+    lib = N.load()
+    assert lib.gs_project_forward(None, None) == 1
+    assert b"null" in lib.gs_last_error()
+    alt = C.c_int32(0)
+    assert lib.gs_radix_sort_pairs(None, None, None, None, 10, 0, 40, 0, None, 0, C.byref(alt), None) == 1
+    a = N.GsProjectArgs()
+    a.cam.tile_size = 32
+    a.cam.image_width = a.cam.image_height = 8
+    assert lib.gs_project_forward(C.byref(a), None) == 3  # unsupported tile size
+    with pytest.raises(RuntimeError, match="gs_status=3"):
+        N.check(lib.gs_project_forward(C.byref(a), None), "gs_project_forward")
+
+
+def test_workspace_queries(pkg):
+    lib = pkg._native.load()
+    assert lib.gs_radix_sort_workspace_bytes(4096 * 3) >= 4 * (256 * 3 + 256)
+    assert lib.gs_bin_workspace_bytes(1) >= 4

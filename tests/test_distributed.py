@@ -1,0 +1,64 @@
+"""Data-parallel grad all-reduce over gloo, world_size 2, CPU."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = pkg.GaussianModel()
+        m.create_from_random(100, generator=torch.Generator().manual_seed(0))  # identical replicas
+        params = m.grad_parameters()
+        g = torch.Generator().manual_seed(100 + rank)
+        for i, p in enumerate(params):
+            if rank == 1 and i == 4:
+                p.grad = None  # a rank whose view produced no grad for a param
+            else:
+                p.grad = torch.randn(p.shape, generator=g)
+        local = [None if p.grad is None else p.grad.clone() for p in params]
+        red = pkg.distributed.GradAllReduce(params, dist)
+        red.all_reduce_mean()
+        q.put((rank, local, [p.grad.clone() for p in params]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_all_reduce_mean_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict()
+    for _ in range(2):
+        r, local, reduced = q.get(timeout=120)
+        res[r] = (local, reduced)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i in range(5):
+        a = res[0][0][i]
+        b = res[1][0][i] if res[1][0][i] is not None else torch.zeros_like(a)
+        exp = (a + b) / 2
+        assert torch.allclose(res[0][1][i], exp, atol=1e-6)
+        assert torch.equal(res[0][1][i], res[1][1][i])  # replicas stay identical

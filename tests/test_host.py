@@ -1,0 +1,99 @@
+"""Host-side logic of the drop-in API (no GPU needed)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+
+class _Cam:
+    _width, _height, _FoVx, _FoVy = 48, 32, math.radians(70), math.radians(50)
+
+    def world_view_transform(self):
+        m = torch.eye(4)
+        m[:3, 3] = torch.tensor([0.1, 0.2, 0.3])
+        return m
+
+
+def test_camera_params_follow_reference_intrinsics(pkg):
+    """renderer.py:140-152: fx = 0.5 W / tan(FoVx/2) from the CAMERA size,
+    image size from the SETTINGS."""
+    st = pkg.RenderSettings(image_height=20, image_width=30, bg_color=torch.tensor([0.1, 0.2, 0.3]))
+    c = pkg.camera_params(_Cam(), st)
+    assert (c.image_width, c.image_height) == (30, 20)
+    assert c.fx == pytest.approx(0.5 * 48 / math.tan(math.radians(35)))
+    assert c.fy == pytest.approx(0.5 * 32 / math.tan(math.radians(25)))
+    assert (c.cx, c.cy) == (24.0, 16.0)
+    assert c.view[3] == pytest.approx(0.1) and c.view[7] == pytest.approx(0.2) and c.view[11] == pytest.approx(0.3)
+    assert c.tiles_x == 2 and c.tiles_y == 2
+    assert c.bg == pytest.approx((0.1, 0.2, 0.3))
+
+
+def test_world_view_as_tensor_attribute(pkg):
+    class Cam2(_Cam):
+        pass
+    cam = Cam2()
+    cam.world_view_transform = torch.eye(4)
+    c = pkg.camera_params(cam, pkg.RenderSettings(8, 8, torch.zeros(3)))
+    assert c.view == tuple([1.0, 0, 0, 0, 0, 1.0, 0, 0, 0, 0, 1.0, 0])
+
+
+def test_no_cpu_fallback(pkg):
+    """The product path must fail loudly without a HIP device tensor."""
+    m = pkg.GaussianModel()
+    m.create_from_random(10)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        pkg.GaussianRenderer().render(_Cam(), m, pkg.RenderSettings(8, 8, torch.zeros(3)))
+
+
+def test_tile_size_must_be_16(pkg):
+    with pytest.raises(ValueError):
+        pkg.GaussianRenderer(tile_size=8)
+
+
+def test_gaussian_model_layout(pkg):
+    """test_gaussian_model.py:35-72 restated for this package's model."""
+    m = pkg.GaussianModel()
+    m.create_from_random(64, 1.0, generator=torch.Generator().manual_seed(0))
+    assert m._xyz.shape == (64, 3) and m._features_dc.shape == (64, 1, 3)
+    assert m._features_rest.shape == (64, 15, 3) and m._scaling.shape == (64, 3)
+    assert m._rotation.shape == (64, 4) and m._opacity.shape == (64, 1)
+    assert m.get_features.shape == (64, 16, 3)
+    assert torch.all(m.get_scaling > 0)
+    assert torch.allclose(m.get_rotation.norm(dim=-1), torch.ones(64), atol=1e-5)
+    a = m.get_opacity
+    assert torch.all(a > 0) and torch.all(a < 1)
+
+
+def test_covariance_property_works(pkg):
+    """Reference get_covariance is broken (gaussian_model.py:127); ours equals
+    compute_3d_covariance and the oracle's restatement."""
+    import golden_io as G
+    m = pkg.GaussianModel()
+    m.create_from_random(32, generator=torch.Generator().manual_seed(1))
+    cov = m.get_covariance.detach().numpy()
+    ref = G.oracle().covariance(m._scaling.detach().numpy(), m._rotation.detach().numpy())
+    assert np.allclose(cov, ref, atol=1e-6, rtol=1e-5)
+
+
+def test_camera_world_view_matches_reference_producer(pkg):
+    """CameraUtils.build_world_view_matrix (camera.py:80-141): C2W -> W2C."""
+    ang = 0.4
+    R = np.array([[math.cos(ang), -math.sin(ang), 0], [math.sin(ang), math.cos(ang), 0], [0, 0, 1]], np.float32)
+    C = np.array([1.0, -2.0, 0.5], np.float32)
+    cam = pkg.Camera(0, R, C, 1.0, 1.0, None, "x", 16, 16)
+    wv = cam.world_view_transform().numpy()
+    assert np.allclose(wv[:3, :3], R.T, atol=1e-6)
+    assert np.allclose(wv[:3, 3], -R.T @ C, atol=1e-6)
+    assert np.allclose(cam.camera_center.numpy(), C, atol=1e-5)
+
+
+def test_synthetic_scene_distribution(pkg):
+    sc = pkg.synthetic.make_scene(5000, 192, 108, seed=0)
+    z = sc.xyz[:, 2]
+    assert z.min() >= 2 and z.max() <= 6
+    s = sc.scaling.exp()
+    assert s.min() >= 0.002 - 1e-6 and s.max() <= 0.01 + 1e-6
+    assert torch.allclose(sc.rotation.norm(dim=1), torch.ones(5000), atol=1e-5)
+    sc2 = pkg.synthetic.make_scene(5000, 192, 108, seed=0)
+    assert torch.equal(sc.xyz, sc2.xyz)
