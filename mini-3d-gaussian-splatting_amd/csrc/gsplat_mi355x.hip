@@ -94,25 +94,6 @@ __device__ __forceinline__ unsigned long long match_digit(uint32_t d, int nbits,
   return m;
 }
 
-// ------------------------------------------------------ wave reductions ----
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-// Sum over the 64 lanes; every lane must be active.  Row sums via DPP
-// (quad_perm, row_ror), then the four row totals via readlane.
-__device__ __forceinline__ float wave_sum(float v) {
-  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp<0x124>(v);  // row_ror:4
-  v += dpp<0x128>(v);  // row_ror:8
-  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-  return (r0 + r1) + (r2 + r3);
-}
-
 // ------------------------------------------------------------ geometry ----
 __device__ __forceinline__ void unpack_rect(const uint32_t *rects, uint32_t g, int &tx0, int &tx1,
                                             int &ty0, int &ty1) {
@@ -473,6 +454,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         const float4 r1 = s_r1[j];
         const float dx = fx - r0.x, dy = fy - r0.y;
         const float s = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;  // :333
+        if (s > 23.1f) continue;  // exp(-11.55) < 1e-5: the :336 skip, decided without exp
         const float w = clamp01(expf(-0.5f * s));                                 // :334
         if (w < kMinWeight) continue;                                            // :336
         const float ai = clamp01(r1.y * w);                                      // :339
@@ -508,20 +490,47 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
 }
 
 // ======================================================== blend bwd =======
+// Two phases per batch of kBwdBatch list entries, so that no per-pair
+// cross-lane reduction is needed:
+//  A (pixel-parallel): every pixel replays its front-to-back chain over the
+//    batch -- bit-identical to the forward's decisions -- and writes three
+//    scalars per (entry, pixel) to LDS: ds = dL/ds (the quadratic form),
+//    dop = dL/d opacity, c = the pixel's contribution weight.
+//  B (entry-parallel): each 16-lane row owns one entry, sums its 256 pixels
+//    (16 per lane) into the 10 gradient values, reduces the row with DPP and
+//    writes the entry's slot.
+constexpr int kBwdBatch = 16;
+constexpr int kPdStride = kBlock + 16;  // rows of the pair arrays: +16 floats keeps 16-lane rows on disjoint banks
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_row(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// Sum over the 16 lanes of each DPP row; every lane of the row gets the sum.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_row<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_row<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_row<0x124>(v);  // row_ror:4
+  v += dpp_row<0x128>(v);  // row_ror:8
+  return v;
+}
+
 __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
-  __shared__ float4 s_r0[kBlock], s_r1[kBlock], s_r2[kBlock];
-  __shared__ uint32_t s_e[kBlock];
-  __shared__ float s_red[4][kBlock * GS_PAIR_GRAD_FLOATS];
+  __shared__ float4 s_r0[kBwdBatch], s_r1[kBwdBatch], s_r2[kBwdBatch];
+  __shared__ uint32_t s_e[kBwdBatch];
+  __shared__ float s_ds[kBwdBatch][kPdStride], s_dop[kBwdBatch][kPdStride], s_c[kBwdBatch][kPdStride];
+  __shared__ float4 s_pg[kBlock];   // per pixel: dL/drgb (masked), dL/dD
+  __shared__ float2 s_pxy[kBlock];  // per pixel: integer coordinates as float
   __shared__ uint32_t s_max;
   const int tile = blockIdx.x;
+  const int tid = threadIdx.x;
   int px, py;
   tile_pixel(tile, a.tiles_x, px, py);
   const int W = a.cam.image_width, H = a.cam.image_height;
   const bool inside = px < W && py < H;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t start = a.ranges[2 * tile], end = a.ranges[2 * tile + 1];
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
-  if (threadIdx.x == 0) s_max = 0;
+  if (tid == 0) s_max = 0;
   // pixel cotangents through clamp / bg composite / depth normalisation
   float gR0 = 0.f, gR1 = 0.f, gR2 = 0.f, gA = 0.f, gD = 0.f;
   float tr = 0.f, tg = 0.f, tbl = 0.f, Dt = 0.f, At = 0.f;
@@ -546,108 +555,112 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       gA += -a.g_depth[p] * Dt / (den * den);
     }
   }
+  const float fx = (float)px, fy = (float)py;
+  s_pg[tid] = make_float4(gR0, gR1, gR2, gD);
+  s_pxy[tid] = make_float2(fx, fy);
   __syncthreads();
   if (neval) atomicMax(&s_max, neval);
   __syncthreads();
   const uint32_t stop = start + s_max;
-  const float fx = (float)px, fy = (float)py;
   const float onemA = 1.f - At;
   float A = 0.f, D = 0.f, ar = bg0, ag = bg1, ab = bg2;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
-  for (uint32_t b = start; b < stop; b += kBlock) {
-    const uint32_t cnt = min((uint32_t)kBlock, stop - b);
-    __syncthreads();  // previous batch's s_red / records consumed
-    if (threadIdx.x < cnt) {
-      const uint32_t gid = a.sorted_gauss[b + threadIdx.x];
-      s_r0[threadIdx.x] = recs[3 * (size_t)gid];
-      s_r1[threadIdx.x] = recs[3 * (size_t)gid + 1];
-      s_r2[threadIdx.x] = recs[3 * (size_t)gid + 2];
-      s_e[threadIdx.x] = a.sorted_pairs[b + threadIdx.x];
+  const int jj = tid >> 4, sub = tid & 15;  // phase B: row jj owns entry jj
+  for (uint32_t b = start; b < stop; b += kBwdBatch) {
+    const uint32_t cnt = min((uint32_t)kBwdBatch, stop - b);
+    __syncthreads();  // previous phase B done with s_r*, s_ds, s_dop, s_c
+    if (tid < cnt) {
+      const uint32_t gid = a.sorted_gauss[b + tid];
+      s_r0[tid] = recs[3 * (size_t)gid];
+      s_r1[tid] = recs[3 * (size_t)gid + 1];
+      s_r2[tid] = recs[3 * (size_t)gid + 2];
+      s_e[tid] = a.sorted_pairs[b + tid];
     }
     __syncthreads();
+    // ---- phase A: replay ------------------------------------------------
     const uint32_t jbase = b - start;
     for (uint32_t j = 0; j < cnt; ++j) {
-      float gv[GS_PAIR_GRAD_FLOATS];
-#pragma unroll
-      for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) gv[k] = 0.f;
-      bool contributed = false;
+      float ds = 0.f, dop = 0.f, cw = 0.f;
       if (jbase + j < neval) {
         const float4 r0 = s_r0[j];
         const float4 r1 = s_r1[j];
         const float dx = fx - r0.x, dy = fy - r0.y;
-        const float s = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;
-        const float e = expf(-0.5f * s);
-        const float w = clamp01(e);
-        if (w >= kMinWeight) {
+        const float sq = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;
+        if (!(sq > 23.1f)) {  // exp(-11.55) < 1e-5: exact early skip (NaN falls through)
+          const float e = expf(-0.5f * sq);
+          const float w = clamp01(e);
           const float u = r1.y * w;
           const float ai = clamp01(u);
-          if (ai > 0.f) {
-            const float trans = 1.f - A;
-            const float c = trans * ai;
-            if (c > 0.f) {
-              contributed = true;
-              const float4 r2 = s_r2[j];
-              ar += c * r2.x;
-              ag += c * r2.y;
-              ab += c * r2.z;
-              A = A + c;
-              D += c * r1.z;
-              const float Tn = 1.f - A;
-              float dal;
-              if (Tn == 0.f) {
-                dal = trans * (gR0 * r2.x + gR1 * r2.y + gR2 * r2.z + gD * r1.z + gA);
-              } else {
-                const float inv = 1.f / Tn;
-                const float sr = gR0 * (r2.x - (tr - ar) * inv) + gR1 * (r2.y - (tg - ag) * inv) +
-                                 gR2 * (r2.z - (tbl - ab) * inv) + gD * (r1.z - (Dt - D) * inv) +
-                                 gA * (onemA * inv);
-                dal = trans * sr;
-              }
-              const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
-              const float dw = du * r1.y;
-              const float de = (e >= 0.f && e <= 1.f) ? dw : 0.f;
-              const float ds = de * e * -0.5f;
-              gv[0] = -ds * (2.f * dx * r0.z + r0.w * dy);
-              gv[1] = -ds * (r0.w * dx + 2.f * dy * r1.x);
-              gv[2] = ds * dx * dx;
-              gv[3] = ds * dx * dy;
-              gv[4] = ds * dy * dy;
-              gv[5] = du * w;
-              gv[6] = gR0 * c;
-              gv[7] = gR1 * c;
-              gv[8] = gR2 * c;
-              gv[9] = gD * c;
+          const float trans = 1.f - A;
+          const float c = trans * ai;
+          if (!(w < kMinWeight) && !(ai <= 0.f) && !(c <= 0.f)) {  // the forward's three skips, NaN-exact
+            const float4 r2 = s_r2[j];
+            ar += c * r2.x;
+            ag += c * r2.y;
+            ab += c * r2.z;
+            A = A + c;
+            D += c * r1.z;
+            const float Tn = 1.f - A;
+            float dal;
+            if (Tn == 0.f) {
+              dal = trans * (gR0 * r2.x + gR1 * r2.y + gR2 * r2.z + gD * r1.z + gA);
+            } else {
+              const float inv = __frcp_rn(Tn);
+              const float sr = gR0 * (r2.x - (tr - ar) * inv) + gR1 * (r2.y - (tg - ag) * inv) +
+                               gR2 * (r2.z - (tbl - ab) * inv) + gD * (r1.z - (Dt - D) * inv) +
+                               gA * (onemA * inv);
+              dal = trans * sr;
             }
+            const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
+            const float de = (e >= 0.f && e <= 1.f) ? du * r1.y : 0.f;
+            ds = de * e * -0.5f;
+            dop = du * w;
+            cw = c;
           }
         }
       }
-      float *dst = &s_red[wave][j * GS_PAIR_GRAD_FLOATS];
-      if (__any(contributed)) {
-#pragma unroll
-        for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) {
-          const float v = wave_sum(gv[k]);
-          if (lane == 0) dst[k] = v;
-        }
-      } else if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) dst[k] = 0.f;
-      }
+      s_ds[j][tid] = ds;
+      s_dop[j][tid] = dop;
+      s_c[j][tid] = cw;
     }
     __syncthreads();
-    if (threadIdx.x < cnt) {
-      const int j = threadIdx.x;
-      float *out = a.pair_grads + (size_t)s_e[j] * GS_PAIR_GRAD_FLOATS;
-#pragma unroll
-      for (int k = 0; k < GS_PAIR_GRAD_FLOATS; k += 2) {
-        const int o = j * GS_PAIR_GRAD_FLOATS + k;
-        const float v0 = (s_red[0][o] + s_red[1][o]) + (s_red[2][o] + s_red[3][o]);
-        const float v1 = (s_red[0][o + 1] + s_red[1][o + 1]) + (s_red[2][o + 1] + s_red[3][o + 1]);
-        reinterpret_cast<float2 *>(out)[k / 2] = make_float2(v0, v1);
+    // ---- phase B: per-entry sums ----------------------------------------
+    if ((uint32_t)jj < cnt) {
+      const float4 r0 = s_r0[jj];
+      const float mx = r0.x, my = r0.y, q00 = r0.z, qo = r0.w, q11 = s_r1[jj].x;
+      float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < kBlock / 16; ++k) {
+        const int p = sub + 16 * k;
+        const float ds = s_ds[jj][p], dop = s_dop[jj][p], cw = s_c[jj][p];
+        const float4 pg = s_pg[p];
+        const float2 xy = s_pxy[p];
+        const float dx = xy.x - mx, dy = xy.y - my;
+        g0 += ds * (2.f * dx * q00 + qo * dy);
+        g1 += ds * (qo * dx + 2.f * dy * q11);
+        g2 += ds * dx * dx;
+        g3 += ds * dx * dy;
+        g4 += ds * dy * dy;
+        g5 += dop;
+        g6 += pg.x * cw;
+        g7 += pg.y * cw;
+        g8 += pg.z * cw;
+        g9 += pg.w * cw;
+      }
+      g0 = row16_sum(g0); g1 = row16_sum(g1); g2 = row16_sum(g2); g3 = row16_sum(g3); g4 = row16_sum(g4);
+      g5 = row16_sum(g5); g6 = row16_sum(g6); g7 = row16_sum(g7); g8 = row16_sum(g8); g9 = row16_sum(g9);
+      if (sub == 0) {
+        float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)s_e[jj] * GS_PAIR_GRAD_FLOATS);
+        out[0] = make_float2(-g0, -g1);
+        out[1] = make_float2(g2, g3);
+        out[2] = make_float2(g4, g5);
+        out[3] = make_float2(g6, g7);
+        out[4] = make_float2(g8, g9);
       }
     }
   }
   // entries past every pixel's last evaluated pair carry no gradient
-  for (uint32_t q = stop + threadIdx.x; q < end; q += kBlock) {
+  for (uint32_t q = stop + tid; q < end; q += kBlock) {
     float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)a.sorted_pairs[q] * GS_PAIR_GRAD_FLOATS);
 #pragma unroll
     for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) out[k] = make_float2(0.f, 0.f);
