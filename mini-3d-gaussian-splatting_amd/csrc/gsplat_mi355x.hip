@@ -563,7 +563,12 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   __syncthreads();
   const uint32_t stop = start + s_max;
   const float onemA = 1.f - At;
-  float A = 0.f, D = 0.f, ar = bg0, ag = bg1, ab = bg2;
+  // Suffix sums without per-channel state: with X_i = gR . col_i + gD z_i,
+  //   sum_k gR_k (accT_k - acc_k) + gD (Dt - D) = K - P,
+  //   K = gR . accT + gD Dt (per pixel),  P = gR . acc + gD D (running; acc starts at bg)
+  const float K = (gR0 * tr + gR1 * tg) + (gR2 * tbl + gD * Dt);
+  float P = (gR0 * bg0 + gR1 * bg1) + gR2 * bg2;
+  float A = 0.f;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   const int jj = tid >> 4, sub = tid & 15;  // phase B: row jj owns entry jj
   for (uint32_t b = start; b < stop; b += kBwdBatch) {
@@ -595,21 +600,16 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
           const float c = trans * ai;
           if (!(w < kMinWeight) && !(ai <= 0.f) && !(c <= 0.f)) {  // the forward's three skips, NaN-exact
             const float4 r2 = s_r2[j];
-            ar += c * r2.x;
-            ag += c * r2.y;
-            ab += c * r2.z;
+            const float X = __builtin_fmaf(gR0, r2.x, __builtin_fmaf(gR1, r2.y, __builtin_fmaf(gR2, r2.z, gD * r1.z)));
             A = A + c;
-            D += c * r1.z;
-            const float Tn = 1.f - A;
             float dal;
-            if (Tn == 0.f) {
-              dal = trans * (gR0 * r2.x + gR1 * r2.y + gR2 * r2.z + gD * r1.z + gA);
+            if (A >= kAlphaStop) {
+              // the terminating contributor: nothing behind it, (1-A_total)/T_{i+1} = 1
+              dal = trans * (X + gA);
             } else {
-              const float inv = __frcp_rn(Tn);
-              const float sr = gR0 * (r2.x - (tr - ar) * inv) + gR1 * (r2.y - (tg - ag) * inv) +
-                               gR2 * (r2.z - (tbl - ab) * inv) + gD * (r1.z - (Dt - D) * inv) +
-                               gA * (onemA * inv);
-              dal = trans * sr;
+              P = __builtin_fmaf(c, X, P);
+              const float inv = __frcp_rn(1.f - A);
+              dal = trans * __builtin_fmaf(inv, __builtin_fmaf(gA, onemA, P - K), X);
             }
             const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
             const float de = (e >= 0.f && e <= 1.f) ? du * r1.y : 0.f;
@@ -627,8 +627,9 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
     // ---- phase B: per-entry sums ----------------------------------------
     if ((uint32_t)jj < cnt) {
       const float4 r0 = s_r0[jj];
-      const float mx = r0.x, my = r0.y, q00 = r0.z, qo = r0.w, q11 = s_r1[jj].x;
-      float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
+      const float mx = r0.x, my = r0.y;
+      // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy) with Sx = sum ds dx, Sy = sum ds dy
+      float Sx = 0.f, Sy = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
 #pragma unroll 4
       for (int k = 0; k < kBlock / 16; ++k) {
         const int p = sub + 16 * k;
@@ -636,22 +637,25 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         const float4 pg = s_pg[p];
         const float2 xy = s_pxy[p];
         const float dx = xy.x - mx, dy = xy.y - my;
-        g0 += ds * (2.f * dx * q00 + qo * dy);
-        g1 += ds * (qo * dx + 2.f * dy * q11);
-        g2 += ds * dx * dx;
-        g3 += ds * dx * dy;
-        g4 += ds * dy * dy;
+        const float t = ds * dx, v = ds * dy;
+        Sx += t;
+        Sy += v;
+        g2 = __builtin_fmaf(t, dx, g2);
+        g3 = __builtin_fmaf(t, dy, g3);
+        g4 = __builtin_fmaf(v, dy, g4);
         g5 += dop;
-        g6 += pg.x * cw;
-        g7 += pg.y * cw;
-        g8 += pg.z * cw;
-        g9 += pg.w * cw;
+        g6 = __builtin_fmaf(pg.x, cw, g6);
+        g7 = __builtin_fmaf(pg.y, cw, g7);
+        g8 = __builtin_fmaf(pg.z, cw, g8);
+        g9 = __builtin_fmaf(pg.w, cw, g9);
       }
-      g0 = row16_sum(g0); g1 = row16_sum(g1); g2 = row16_sum(g2); g3 = row16_sum(g3); g4 = row16_sum(g4);
+      Sx = row16_sum(Sx); Sy = row16_sum(Sy); g2 = row16_sum(g2); g3 = row16_sum(g3); g4 = row16_sum(g4);
       g5 = row16_sum(g5); g6 = row16_sum(g6); g7 = row16_sum(g7); g8 = row16_sum(g8); g9 = row16_sum(g9);
       if (sub == 0) {
+        const float q00 = r0.z, qo = r0.w, q11 = s_r1[jj].x;
+        const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
         float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)s_e[jj] * GS_PAIR_GRAD_FLOATS);
-        out[0] = make_float2(-g0, -g1);
+        out[0] = make_float2(g0, g1);
         out[1] = make_float2(g2, g3);
         out[2] = make_float2(g4, g5);
         out[3] = make_float2(g6, g7);
