@@ -454,23 +454,26 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         const float4 r1 = s_r1[j];
         const float dx = fx - r0.x, dy = fy - r0.y;
         const float s = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;  // :333
-        if (s > 23.1f) continue;  // exp(-11.55) < 1e-5: the :336 skip, decided without exp
-        const float w = clamp01(expf(-0.5f * s));                                 // :334
-        if (w < kMinWeight) continue;                                            // :336
-        const float ai = clamp01(r1.y * w);                                      // :339
-        if (ai <= 0.f) continue;
-        const float c = (1.f - A) * ai;                                          // :343-344
-        if (c <= 0.f) continue;
-        const float4 r2 = s_r2[j];
-        ar += c * r2.x;
-        ag += c * r2.y;
-        ab += c * r2.z;
-        A = A + c;
-        D += c * r1.z;
-        if (A >= kAlphaStop) {  // :352 (after accumulation)
-          done = true;
-          neval = b - start + j + 1;
-          break;
+        // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp;
+        // the branch is taken by the whole wave or the exp is predicated.
+        if (!(s > 23.1f)) {
+          const float w = clamp01(expf(-0.5f * s));  // :334
+          const float ai = clamp01(r1.y * w);        // :339
+          const float c0 = (1.f - A) * ai;           // :343-344
+          // :336 / :340 / :345 skips as a predicate; a skipped pair adds exact zeros
+          const bool take = !(w < kMinWeight) && !(ai <= 0.f) && !(c0 <= 0.f);
+          const float c = take ? c0 : 0.f;
+          const float4 r2 = s_r2[j];
+          ar += c * r2.x;
+          ag += c * r2.y;
+          ab += c * r2.z;
+          A = A + c;
+          D += c * r1.z;
+          if (take && A >= kAlphaStop) {  // :352 (after accumulation)
+            done = true;
+            neval = b - start + j + 1;
+            break;
+          }
         }
       }
     }
@@ -493,9 +496,10 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
 // Two phases per batch of kBwdBatch list entries, so that no per-pair
 // cross-lane reduction is needed:
 //  A (pixel-parallel): every pixel replays its front-to-back chain over the
-//    batch -- bit-identical to the forward's decisions -- and writes three
-//    scalars per (entry, pixel) to LDS: ds = dL/ds (the quadratic form),
-//    dop = dL/d opacity, c = the pixel's contribution weight.
+//    batch -- bit-identical to the forward's decisions -- and writes two
+//    scalars per (entry, pixel) to LDS: dop = dL/d opacity and the
+//    contribution weight c, whose sign bit flags "exp(-s/2) <= 1" (then
+//    dL/ds = -0.5 * opacity * dop; otherwise the weight clamp blocks it).
 //  B (entry-parallel): each 16-lane row owns one entry, sums its 256 pixels
 //    (16 per lane) into the 10 gradient values, reduces the row with DPP and
 //    writes the entry's slot.
@@ -518,9 +522,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float4 s_r0[kBwdBatch], s_r1[kBwdBatch], s_r2[kBwdBatch];
   __shared__ uint32_t s_e[kBwdBatch];
-  __shared__ float s_ds[kBwdBatch][kPdStride], s_dop[kBwdBatch][kPdStride], s_c[kBwdBatch][kPdStride];
+  __shared__ float s_dop[kBwdBatch][kPdStride], s_c[kBwdBatch][kPdStride];
   __shared__ float4 s_pg[kBlock];   // per pixel: dL/drgb (masked), dL/dD
-  __shared__ float2 s_pxy[kBlock];  // per pixel: integer coordinates as float
   __shared__ uint32_t s_max;
   const int tile = blockIdx.x;
   const int tid = threadIdx.x;
@@ -557,7 +560,6 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   }
   const float fx = (float)px, fy = (float)py;
   s_pg[tid] = make_float4(gR0, gR1, gR2, gD);
-  s_pxy[tid] = make_float2(fx, fy);
   __syncthreads();
   if (neval) atomicMax(&s_max, neval);
   __syncthreads();
@@ -573,7 +575,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   const int jj = tid >> 4, sub = tid & 15;  // phase B: row jj owns entry jj
   for (uint32_t b = start; b < stop; b += kBwdBatch) {
     const uint32_t cnt = min((uint32_t)kBwdBatch, stop - b);
-    __syncthreads();  // previous phase B done with s_r*, s_ds, s_dop, s_c
+    __syncthreads();  // previous phase B done with s_r*, s_dop, s_c
     if (tid < cnt) {
       const uint32_t gid = a.sorted_gauss[b + tid];
       s_r0[tid] = recs[3 * (size_t)gid];
@@ -585,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
     // ---- phase A: replay ------------------------------------------------
     const uint32_t jbase = b - start;
     for (uint32_t j = 0; j < cnt; ++j) {
-      float ds = 0.f, dop = 0.f, cw = 0.f;
+      float dop = 0.f, cw = 0.f;
       if (jbase + j < neval) {
         const float4 r0 = s_r0[j];
         const float4 r1 = s_r1[j];
@@ -612,14 +614,11 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
               dal = trans * __builtin_fmaf(inv, __builtin_fmaf(gA, onemA, P - K), X);
             }
             const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
-            const float de = (e >= 0.f && e <= 1.f) ? du * r1.y : 0.f;
-            ds = de * e * -0.5f;
             dop = du * w;
-            cw = c;
+            cw = (e >= 0.f && e <= 1.f) ? c : -c;
           }
         }
       }
-      s_ds[j][tid] = ds;
       s_dop[j][tid] = dop;
       s_c[j][tid] = cw;
     }
@@ -627,16 +626,21 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
     // ---- phase B: per-entry sums ----------------------------------------
     if ((uint32_t)jj < cnt) {
       const float4 r0 = s_r0[jj];
-      const float mx = r0.x, my = r0.y;
+      const float4 r1 = s_r1[jj];
+      const float mx = r0.x, my = r0.y, hop = -0.5f * r1.y;
+      // pixel p = sub + 16k sits at (tile_x0 + 8((k>>2)&1) + (sub&7), tile_y0 + 8(k>>3) + 2(k&3) + (sub>>3))
+      const float bx = (float)((tile % a.tiles_x) * GS_TILE + (sub & 7)) - mx;
+      const float by = (float)((tile / a.tiles_x) * GS_TILE + (sub >> 3)) - my;
       // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy) with Sx = sum ds dx, Sy = sum ds dy
       float Sx = 0.f, Sy = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
-#pragma unroll 4
+#pragma unroll
       for (int k = 0; k < kBlock / 16; ++k) {
         const int p = sub + 16 * k;
-        const float ds = s_ds[jj][p], dop = s_dop[jj][p], cw = s_c[jj][p];
+        const float dop = s_dop[jj][p], cs = s_c[jj][p];
         const float4 pg = s_pg[p];
-        const float2 xy = s_pxy[p];
-        const float dx = xy.x - mx, dy = xy.y - my;
+        const float dx = bx + (float)(8 * ((k >> 2) & 1)), dy = by + (float)(8 * (k >> 3) + 2 * (k & 3));
+        const float cw = fabsf(cs);
+        const float ds = cs > 0.f ? hop * dop : 0.f;
         const float t = ds * dx, v = ds * dy;
         Sx += t;
         Sy += v;
@@ -652,7 +656,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       Sx = row16_sum(Sx); Sy = row16_sum(Sy); g2 = row16_sum(g2); g3 = row16_sum(g3); g4 = row16_sum(g4);
       g5 = row16_sum(g5); g6 = row16_sum(g6); g7 = row16_sum(g7); g8 = row16_sum(g8); g9 = row16_sum(g9);
       if (sub == 0) {
-        const float q00 = r0.z, qo = r0.w, q11 = s_r1[jj].x;
+        const float q00 = r0.z, qo = r0.w, q11 = r1.x;
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
         float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)s_e[jj] * GS_PAIR_GRAD_FLOATS);
         out[0] = make_float2(g0, g1);
