@@ -34,6 +34,7 @@ extern "C" {
 #define GS_ABI_VERSION 1
 #define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
+#define GS_MAX_RECT_TILES 8   /* r <= 50 px -> an AABB spans at most 8 tiles per axis */
 #define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian) gradient slot */
 #define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2..3] reserved */
 
@@ -84,8 +85,8 @@ typedef struct gs_gaussians {
  * Replaces renderer.py:117-200 and :201-220.  One thread per Gaussian.
  * Writes the render() outputs means2d (viewspace_points), conics, radii and
  * visibility_filter, plus the splat record, tile rectangle and depth sort
- * key used by the later stages.  counters[0] receives M (visible count);
- * the callee zeroes counters first. */
+ * key used by the later stages.  No atomics, no counters: the visible
+ * count is produced by gs_bin_count. */
 typedef struct gs_project_args {
   gs_camera cam;
   gs_gaussians g;
@@ -96,7 +97,6 @@ typedef struct gs_project_args {
   float *records;       /* [n, GS_RECORD_FLOATS] */
   uint32_t *rects;      /* [n,2] packed tile rectangle */
   uint32_t *depth_keys; /* [n]   fp32 bits of Z if visible, else 0xFFFFFFFF */
-  uint32_t *counters;   /* [GS_NUM_COUNTERS] */
 } gs_project_args;
 gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream);
 
@@ -116,17 +116,20 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
                               gs_stream_t stream);
 
 /* ---- Stage 3: tile binning (renderer.py:263-298) ----------------------
- * gs_bin_count: per-Gaussian tile-touch counts in depth order, reduced to
- *   per-block partial sums and scanned; counters[1] receives T.
- * gs_bin_emit : one (tile id, pair index) entry per touched tile, emitted in
- *   depth order (so a stable sort by tile keeps depth order inside a tile);
- *   pair_gauss[e] = Gaussian of entry e, pair_offset[g] = first entry of g. */
+ * gs_bin_count: per-Gaussian tile-touch counts and visibility in depth order,
+ *   reduced to per-block partial sums and scanned; the callee zeroes
+ *   counters, then counters[0] = M (visible), counters[1] = T (touches).
+ * gs_bin_emit : one (tile id, Gaussian id) entry per touched tile, emitted in
+ *   depth order (so a stable sort by tile keeps depth order inside a tile),
+ *   written coalesced; pair_offset[g] = first entry of g, also stored in the
+ *   Gaussian's record (word 7) for the backward's slot addressing. */
 size_t gs_bin_workspace_bytes(int32_t n);
 typedef struct gs_bin_args {
   int32_t n;
   int32_t tiles_x, tiles_y;
   const uint32_t *sorted_ids; /* [n] depth-sorted Gaussian ids (visible first) */
   const uint32_t *rects;      /* [n,2] from gs_project_forward */
+  const uint8_t *vis;         /* [n]   from gs_project_forward */
   uint32_t *counters;         /* [GS_NUM_COUNTERS] */
   void *workspace;
   size_t workspace_bytes;
@@ -134,20 +137,18 @@ typedef struct gs_bin_args {
   uint32_t *tile_keys;   /* [T] */
   uint32_t *pair_gauss;  /* [T] */
   uint32_t *pair_offset; /* [n] indexed by Gaussian id */
+  float *records;        /* [n, GS_RECORD_FLOATS]: word 7 <- pair_offset bits */
 } gs_bin_args;
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream);
 gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream);
 
-/* Per-tile [start,end) ranges of the tile-sorted entries, and the Gaussian
- * id of each sorted entry.  Replaces the tile_lists of renderer.py:266. */
+/* Per-tile [start,end) ranges of the tile-sorted entries.  Replaces the
+ * tile_lists of renderer.py:266 (the sorted values are the Gaussian ids). */
 typedef struct gs_range_args {
   int32_t num_pairs;           /* T */
   int32_t num_tiles;
   const uint32_t *sorted_keys; /* [T] tile ids, sorted */
-  const uint32_t *sorted_pairs;/* [T] entry index e, in tile-sorted order */
-  const uint32_t *pair_gauss;  /* [T] */
   uint32_t *ranges;            /* [num_tiles,2] */
-  uint32_t *sorted_gauss;      /* [T] */
 } gs_range_args;
 gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream);
 
@@ -176,14 +177,14 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
  * Re-walks each pixel's list front-to-back (bit-identical replay of the
  * forward's decisions) and writes one gradient slot per (tile, Gaussian)
  * entry: pair_grads[e] = {dmu_x, dmu_y, dQ00, dQ01(=dQ10), dQ11, d_opacity,
- * d_r, d_g, d_b, d_z}.  No atomics: deterministic. */
+ * d_r, d_g, d_b, d_z}, e = the entry's emit index (pair_offset[g] + its
+ * tile's index in g's rectangle).  No atomics: deterministic. */
 typedef struct gs_blend_bwd_args {
   gs_camera cam;
   int32_t tiles_x, tiles_y;
   const uint32_t *ranges;
   const uint32_t *sorted_gauss;
-  const uint32_t *sorted_pairs; /* [T] entry index e of each sorted entry */
-  const float *records;
+  const float *records;         /* with pair offsets (gs_bin_emit) */
   const float *pix_acc;
   const float *pix_state;
   const float *g_image;         /* [3,H,W] dL/dimage */

@@ -48,22 +48,21 @@ class GsGaussians(C.Structure):
 class GsProjectArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("g", GsGaussians), ("means2d", _vp), ("conics", _vp), ("radii", _vp),
-        ("vis", _vp), ("records", _vp), ("rects", _vp), ("depth_keys", _vp), ("counters", _vp),
+        ("vis", _vp), ("records", _vp), ("rects", _vp), ("depth_keys", _vp),
     ]
 
 
 class GsBinArgs(C.Structure):
     _fields_ = [
         ("n", C.c_int32), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("sorted_ids", _vp),
-        ("rects", _vp), ("counters", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
-        ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp),
+        ("rects", _vp), ("vis", _vp), ("counters", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
+        ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp), ("records", _vp),
     ]
 
 
 class GsRangeArgs(C.Structure):
     _fields_ = [
-        ("num_pairs", C.c_int32), ("num_tiles", C.c_int32), ("sorted_keys", _vp),
-        ("sorted_pairs", _vp), ("pair_gauss", _vp), ("ranges", _vp), ("sorted_gauss", _vp),
+        ("num_pairs", C.c_int32), ("num_tiles", C.c_int32), ("sorted_keys", _vp), ("ranges", _vp),
     ]
 
 
@@ -78,7 +77,7 @@ class GsBlendFwdArgs(C.Structure):
 class GsBlendBwdArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
-        ("sorted_gauss", _vp), ("sorted_pairs", _vp), ("records", _vp), ("pix_acc", _vp),
+        ("sorted_gauss", _vp), ("records", _vp), ("pix_acc", _vp),
         ("pix_state", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp),
         ("pair_grads", _vp),
     ]

@@ -25,8 +25,8 @@ constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
-constexpr int kSortIpt = 16;                     // items per thread per sort block
-constexpr int kSortChunk = kBlock * kSortIpt;    // 4096 items per block
+constexpr int kSortIpt = 8;                      // items per thread per sort block
+constexpr int kSortChunk = kBlock * kSortIpt;    // 2048 items per block
 constexpr int kBinChunk = kBlock * 16;           // 4096 Gaussians per binning block
 constexpr float kAlphaStop = 0.995f;             // renderer.py:352
 constexpr float kMinWeight = 1e-5f;              // renderer.py:336
@@ -205,6 +205,7 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
     a.vis[g] = visible ? 1 : 0;
     // tile rectangle (:278-293), int() truncation toward zero
     uint32_t rx = 1u, ry = 1u;  // empty: tx0=1 > tx1=0
+    uint32_t rinfo = 0u;        // record word 11: tx0 | ty0 << 12 | (tiles wide - 1) << 24
     if (visible) {
       const int ri = (int)r, icx = (int)mx, icy = (int)my;
       int x0 = icx - ri, x1 = icx + 1 + ri, y0 = icy - ri, y1 = icy + 1 + ri;
@@ -216,6 +217,7 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
         const int T = GS_TILE;
         rx = (uint32_t)(x0 / T) | ((uint32_t)((x1 - 1) / T) << 16);
         ry = (uint32_t)(y0 / T) | ((uint32_t)((y1 - 1) / T) << 16);
+        rinfo = (uint32_t)(x0 / T) | ((uint32_t)(y0 / T) << 12) | ((uint32_t)((x1 - 1) / T - x0 / T) << 24);
       }
       const float *cl = a.g.color_logits + (int64_t)g * a.g.color_stride;
       const float op = a.g.opacity[(int64_t)g * a.g.opacity_stride];
@@ -223,22 +225,21 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
       rec[0] = make_float4(mx, my, q0, q1 + q2);
       rec[1] = make_float4(q3, op, Z, 0.f);
       rec[2] = make_float4(1.f / (1.f + expf(-cl[0])), 1.f / (1.f + expf(-cl[1])),
-                           1.f / (1.f + expf(-cl[2])), 0.f);  // sigmoid (:90)
+                           1.f / (1.f + expf(-cl[2])), __uint_as_float(rinfo));  // sigmoid (:90)
     }
     reinterpret_cast<uint2 *>(a.rects)[g] = make_uint2(rx, ry);
     a.depth_keys[g] = visible ? __float_as_uint(Z) : 0xFFFFFFFFu;
   }
-  const unsigned long long b = __ballot(visible);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&a.counters[0], (uint32_t)__popcll(b));
 }
 
 // ===================================================== radix sort =========
 // Pass p sorts digit (key >> shift) & mask.  One block = kSortChunk items;
-// wave w owns the contiguous quarter [w*1024, (w+1)*1024) of the chunk,
-// walked in 16 rounds of 64 (order = wave, round, lane: stable).
+// wave w owns the contiguous quarter of the chunk, walked in kSortIpt rounds
+// of 64 (order = wave, round, lane: stable).  No global atomics: per-block
+// digit counts -> per-digit row scan (+ row totals) -> the scatter derives
+// the digit bases from the 256 totals itself.
 __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restrict__ keys, int n, int shift,
-                                                       int nbits, uint32_t *counts, uint32_t *digit_total,
-                                                       int nb) {
+                                                       int nbits, uint32_t *counts, int nb) {
   __shared__ uint32_t hist[kRadix];
   hist[threadIdx.x] = 0;
   __syncthreads();
@@ -253,21 +254,15 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restric
     if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(m));
   }
   __syncthreads();
-  const uint32_t h = hist[threadIdx.x];
-  counts[(size_t)threadIdx.x * nb + blockIdx.x] = h;
-  if (h) atomicAdd(&digit_total[threadIdx.x], h);
+  counts[(size_t)threadIdx.x * nb + blockIdx.x] = hist[threadIdx.x];
 }
 
-// counts[d][b] -> global exclusive offsets; one block per digit.
-__global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, const uint32_t *digit_total, int nb) {
+// row d of counts -> exclusive prefix over blocks; totals[d] = row sum.
+__global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, uint32_t *totals, int nb) {
   __shared__ uint32_t s_tmp[4];
   const int d = blockIdx.x;
-  uint32_t tot;
-  const uint32_t mine = threadIdx.x < (unsigned)d ? digit_total[threadIdx.x] : 0u;
-  const uint32_t ex = block_exscan(mine, s_tmp, &tot);
-  (void)ex;
-  uint32_t carry = tot;  // sum of totals of digits < d
   uint32_t *row = counts + (size_t)d * nb;
+  uint32_t carry = 0, tot;
   for (int c = 0; c < nb; c += kBlock) {
     const int i = c + threadIdx.x;
     const uint32_t v = i < nb ? row[i] : 0u;
@@ -275,18 +270,22 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, const u
     if (i < nb) row[i] = carry + e;
     carry += tot;
   }
+  if (threadIdx.x == 0) totals[d] = carry;
 }
 
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
                                                           const uint32_t *__restrict__ vals_in,
                                                           uint32_t *__restrict__ keys_out,
                                                           uint32_t *__restrict__ vals_out, int n, int shift,
-                                                          int nbits, const uint32_t *counts, int nb) {
+                                                          int nbits, const uint32_t *counts,
+                                                          const uint32_t *totals, int nb) {
   __shared__ uint32_t wcnt[4][kRadix];
+  __shared__ uint32_t s_tmp[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0;
-  __syncthreads();
+  uint32_t tot;
+  const uint32_t dbase = block_exscan(totals[threadIdx.x], s_tmp, &tot);  // includes a barrier
   const uint32_t mask = (1u << nbits) - 1u;
   const long long base = (long long)blockIdx.x * kSortChunk + wave * (kSortChunk / 4);
   uint32_t k_[kSortIpt], v_[kSortIpt], rk[kSortIpt];
@@ -308,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
   }
   __syncthreads();
   {
-    uint32_t run = counts[(size_t)threadIdx.x * nb + blockIdx.x];
+    uint32_t run = dbase + counts[(size_t)threadIdx.x * nb + blockIdx.x];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const uint32_t t = wcnt[w][threadIdx.x];
@@ -329,78 +328,97 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
 }
 
 // ======================================================== binning =========
-__global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials) {
+// partials[0..nb): touches per block, partials[nb..2nb): visible per block
+__global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials, int nb) {
   __shared__ uint32_t s_tmp[4];
   const long long base = (long long)blockIdx.x * kBinChunk;
-  uint32_t sum = 0;
+  uint32_t sum = 0, nvis = 0;
   for (int i = 0; i < kBinChunk / kBlock; ++i) {
     const long long k = base + i * kBlock + threadIdx.x;
     if (k < a.n) {
+      const uint32_t g = a.sorted_ids[k];
       int tx0, tx1, ty0, ty1;
-      unpack_rect(a.rects, a.sorted_ids[k], tx0, tx1, ty0, ty1);
+      unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
       sum += rect_touches(tx0, tx1, ty0, ty1);
+      nvis += a.vis[g] ? 1u : 0u;
     }
   }
-  uint32_t tot;
+  uint32_t tot, totv;
   block_exscan(sum, s_tmp, &tot);
-  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+  block_exscan(nvis, s_tmp, &totv);
+  if (threadIdx.x == 0) {
+    partials[blockIdx.x] = tot;
+    partials[nb + blockIdx.x] = totv;
+  }
 }
 
-// exclusive scan of the block partials (single block); counters[1] = T
+// exclusive scan of the touch partials (single block); counters[0] = M, [1] = T
 __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials, int nb, uint32_t *counters) {
   __shared__ uint32_t s_tmp[4];
-  uint32_t carry = 0, tot;
+  uint32_t carry = 0, vis = 0, tot;
   for (int c = 0; c < nb; c += kBlock) {
     const int i = c + threadIdx.x;
     const uint32_t v = i < nb ? partials[i] : 0u;
     const uint32_t e = block_exscan(v, s_tmp, &tot);
     if (i < nb) partials[i] = carry + e;
     carry += tot;
+    block_exscan(i < nb ? partials[nb + i] : 0u, s_tmp, &tot);
+    vis += tot;
   }
-  if (threadIdx.x == 0) counters[1] = carry;
+  if (threadIdx.x == 0) {
+    counters[0] = vis;
+    counters[1] = carry;
+    counters[2] = 0;
+    counters[3] = 0;
+  }
 }
 
+// Emission, coalesced: per round of 256 depth-ordered Gaussians, scan their
+// touch counts into LDS, then every thread writes consecutive output entries,
+// finding its Gaussian by binary search over the round's offsets.
 __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials) {
-  __shared__ uint32_t s_ids[kBinChunk];
+  __shared__ uint32_t s_off[kBlock + 1];
+  __shared__ uint32_t s_g[kBlock];
+  __shared__ uint2 s_rect[kBlock];
   __shared__ uint32_t s_tmp[4];
   const long long base = (long long)blockIdx.x * kBinChunk;
-  for (int i = 0; i < kBinChunk / kBlock; ++i) {
-    const long long k = base + i * kBlock + threadIdx.x;
-    s_ids[i * kBlock + threadIdx.x] = k < a.n ? a.sorted_ids[k] : 0xFFFFFFFFu;
-  }
-  __syncthreads();
-  constexpr int per = kBinChunk / kBlock;  // 16 consecutive items per thread
-  uint32_t cnt[per];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < per; ++j) {
-    const uint32_t g = s_ids[threadIdx.x * per + j];
-    uint32_t t = 0;
+  uint32_t out_base = partials[blockIdx.x];
+  for (int r = 0; r < kBinChunk / kBlock; ++r) {
+    const long long k = base + r * kBlock + threadIdx.x;
+    uint32_t g = 0xFFFFFFFFu, cnt = 0;
+    uint2 rc = make_uint2(1u, 1u);
+    if (k < a.n) {
+      g = a.sorted_ids[k];
+      rc = reinterpret_cast<const uint2 *>(a.rects)[g];
+      cnt = rect_touches((int)(rc.x & 0xFFFFu), (int)(rc.x >> 16), (int)(rc.y & 0xFFFFu), (int)(rc.y >> 16));
+    }
+    uint32_t tot;
+    const uint32_t ex = block_exscan(cnt, s_tmp, &tot);  // barrier inside: previous round done
+    s_off[threadIdx.x] = ex;
+    s_g[threadIdx.x] = g;
+    s_rect[threadIdx.x] = rc;
+    if (threadIdx.x == 0) s_off[kBlock] = tot;
     if (g != 0xFFFFFFFFu) {
-      int tx0, tx1, ty0, ty1;
-      unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
-      t = rect_touches(tx0, tx1, ty0, ty1);
+      a.pair_offset[g] = out_base + ex;
+      if (cnt) a.records[(size_t)g * GS_RECORD_FLOATS + 7] = __uint_as_float(out_base + ex);
     }
-    cnt[j] = t;
-    sum += t;
-  }
-  uint32_t tot;
-  uint32_t off = block_exscan(sum, s_tmp, &tot) + partials[blockIdx.x];
-#pragma unroll
-  for (int j = 0; j < per; ++j) {
-    const uint32_t g = s_ids[threadIdx.x * per + j];
-    if (g == 0xFFFFFFFFu) continue;
-    a.pair_offset[g] = off;
-    if (cnt[j]) {
-      int tx0, tx1, ty0, ty1;
-      unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
-      for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-          a.tile_keys[off] = (uint32_t)(ty * a.tiles_x + tx);
-          a.pair_gauss[off] = g;
-          ++off;
-        }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < tot; o += kBlock) {
+      // last i with s_off[i] <= o (entries with zero touches share offsets)
+      int lo = 0, hi = kBlock;  // invariant: s_off[lo] <= o < s_off[hi]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (s_off[mid] <= o) lo = mid; else hi = mid;
+      }
+      const uint2 rr = s_rect[lo];
+      const uint32_t tx0 = rr.x & 0xFFFFu, ty0 = rr.y & 0xFFFFu;
+      const uint32_t wt = (rr.x >> 16) - tx0 + 1u;
+      const uint32_t loc = o - s_off[lo];
+      const uint32_t row = loc / wt;
+      a.tile_keys[out_base + o] = (ty0 + row) * (uint32_t)a.tiles_x + tx0 + (loc - row * wt);
+      a.pair_gauss[out_base + o] = s_g[lo];
     }
+    out_base += tot;
   }
 }
 
@@ -410,7 +428,6 @@ __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
   const uint32_t t = a.sorted_keys[p];
   if (p == 0 || a.sorted_keys[p - 1] != t) a.ranges[2 * t] = (uint32_t)p;
   if (p == a.num_pairs - 1 || a.sorted_keys[p + 1] != t) a.ranges[2 * t + 1] = (uint32_t)(p + 1);
-  a.sorted_gauss[p] = a.pair_gauss[a.sorted_pairs[p]];
 }
 
 // ======================================================== blend fwd =======
@@ -580,8 +597,13 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       const uint32_t gid = a.sorted_gauss[b + tid];
       s_r0[tid] = recs[3 * (size_t)gid];
       s_r1[tid] = recs[3 * (size_t)gid + 1];
-      s_r2[tid] = recs[3 * (size_t)gid + 2];
-      s_e[tid] = a.sorted_pairs[b + tid];
+      const float4 r2 = recs[3 * (size_t)gid + 2];
+      s_r2[tid] = r2;
+      // emit index of this entry: pair_offset[g] + the tile's index in g's rectangle
+      const uint32_t info = __float_as_uint(r2.w);
+      const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
+      s_e[tid] = __float_as_uint(s_r1[tid].w) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
+                 (tx - (info & 0xFFFu));
     }
     __syncthreads();
     // ---- phase A: replay ------------------------------------------------
@@ -668,8 +690,13 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
     }
   }
   // entries past every pixel's last evaluated pair carry no gradient
+  const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
   for (uint32_t q = stop + tid; q < end; q += kBlock) {
-    float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)a.sorted_pairs[q] * GS_PAIR_GRAD_FLOATS);
+    const uint32_t gid = a.sorted_gauss[q];
+    const float w7 = a.records[(size_t)gid * GS_RECORD_FLOATS + 7];
+    const uint32_t info = __float_as_uint(a.records[(size_t)gid * GS_RECORD_FLOATS + 11]);
+    const uint32_t e = __float_as_uint(w7) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) + (tx - (info & 0xFFFu));
+    float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)e * GS_PAIR_GRAD_FLOATS);
 #pragma unroll
     for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) out[k] = make_float2(0.f, 0.f);
   }
@@ -860,15 +887,11 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   a.d_rotation[4 * (size_t)g + 3] = (float)((dz - z * dot) / qn);
 }
 
+// tile coordinates are packed in 12 bits (record word 11): images up to 65536 px a side
 bool cam_ok(const gs_camera &c) {
   return c.tile_size == GS_TILE && c.image_width > 0 && c.image_height > 0 &&
-         c.image_width < (GS_TILE << 16) && c.image_height < (GS_TILE << 16);
+         c.image_width <= (GS_TILE << 12) && c.image_height <= (GS_TILE << 12);
 }
-
-struct SortWs {
-  uint32_t *counts;
-  uint32_t *digit_total;
-};
 
 }  // namespace
 
@@ -882,10 +905,8 @@ const char *gs_last_error(void) { return g_err; }
 gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_project_forward");
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16 and image size positive", "gs_project_forward");
-  if (a->g.n < 0 || !a->counters) return fail(GS_ERR_INVALID_ARG, "%s: bad n / counters", "gs_project_forward");
+  if (a->g.n < 0) return fail(GS_ERR_INVALID_ARG, "%s: bad n", "gs_project_forward");
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(a->counters, 0, sizeof(uint32_t) * GS_NUM_COUNTERS, s) != hipSuccess)
-    return fail(GS_ERR_LAUNCH, "%s: memset failed", "gs_project_forward");
   if (a->g.n == 0) return GS_OK;
   if (!a->g.xyz || !a->g.color_logits || !a->g.opacity || !a->means2d || !a->conics || !a->radii ||
       !a->vis || !a->records || !a->rects || !a->depth_keys)
@@ -917,17 +938,15 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(n, kSortChunk);
   uint32_t *counts = (uint32_t *)workspace;
-  uint32_t *digit_total = counts + (size_t)kRadix * nb;
+  uint32_t *totals = counts + (size_t)kRadix * nb;
   uint32_t *kin = keys, *vin = vals, *kout = keys_alt, *vout = vals_alt;
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * kRadixBits;
     const int nbits = (end_bit - shift) < kRadixBits ? (end_bit - shift) : kRadixBits;
-    if (hipMemsetAsync(digit_total, 0, sizeof(uint32_t) * kRadix, s) != hipSuccess)
-      return fail(GS_ERR_LAUNCH, "%s: memset failed", "gs_radix_sort_pairs");
-    k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, digit_total, nb);
-    k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, digit_total, nb);
+    k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, nb);
+    k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, totals, nb);
     k_radix_scatter<<<nb, kBlock, 0, s>>>(kin, (p == 0 && vals_are_iota) ? nullptr : vin, kout, vout, n, shift,
-                                          nbits, counts, nb);
+                                          nbits, counts, totals, nb);
     gs_status st = check_launch("gs_radix_sort_pairs");
     if (st) return st;
     uint32_t *tk = kin, *tv = vin;
@@ -940,18 +959,18 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
 }
 
 size_t gs_bin_workspace_bytes(int32_t n) {
-  return sizeof(uint32_t) * (size_t)(n > 0 ? div_up(n, kBinChunk) : 1) + 256;
+  return 2 * sizeof(uint32_t) * (size_t)(n > 0 ? div_up(n, kBinChunk) : 1) + 256;
 }
 
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
   if (!a || !a->counters) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_bin_count");
   if (a->n <= 0) return GS_OK;
-  if (!a->sorted_ids || !a->rects || !a->workspace || a->workspace_bytes < gs_bin_workspace_bytes(a->n))
+  if (!a->sorted_ids || !a->rects || !a->vis || !a->workspace || a->workspace_bytes < gs_bin_workspace_bytes(a->n))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer or workspace too small", "gs_bin_count");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
   uint32_t *partials = (uint32_t *)a->workspace;
-  k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials);
+  k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials, nb);
   k_bin_scan_partials<<<1, kBlock, 0, s>>>(partials, nb, a->counters);
   return check_launch("gs_bin_count");
 }
@@ -959,7 +978,8 @@ gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
 gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_bin_emit");
   if (a->n <= 0) return GS_OK;
-  if (!a->sorted_ids || !a->rects || !a->workspace || !a->tile_keys || !a->pair_gauss || !a->pair_offset)
+  if (!a->sorted_ids || !a->rects || !a->workspace || !a->tile_keys || !a->pair_gauss || !a->pair_offset ||
+      !a->records)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_bin_emit");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
@@ -973,8 +993,7 @@ gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream) {
   if (hipMemsetAsync(a->ranges, 0, sizeof(uint32_t) * 2 * (size_t)a->num_tiles, s) != hipSuccess)
     return fail(GS_ERR_LAUNCH, "%s: memset failed", "gs_tile_ranges");
   if (a->num_pairs <= 0) return GS_OK;
-  if (!a->sorted_keys || !a->sorted_pairs || !a->pair_gauss || !a->sorted_gauss)
-    return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_ranges");
+  if (!a->sorted_keys) return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_ranges");
   k_tile_ranges<<<div_up(a->num_pairs, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_tile_ranges");
 }

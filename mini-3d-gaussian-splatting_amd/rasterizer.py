@@ -122,8 +122,8 @@ def _check_inputs(xyz: torch.Tensor):
 
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
-    __slots__ = ("records", "rects", "vis", "pair_offset", "ranges", "sorted_gauss", "sorted_pairs",
-                 "pix_acc", "pix_state", "M", "T")
+    __slots__ = ("records", "rects", "vis", "pair_offset", "ranges", "sorted_gauss", "pix_acc", "pix_state",
+                 "M", "T")
 
 
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity):
@@ -148,7 +148,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
 
     StageTimer.mark("project_fwd")
     pa = N.GsProjectArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(radii), N.ptr(vis), N.ptr(records),
-                         N.ptr(rects), N.ptr(keys[0]), N.ptr(counters))
+                         N.ptr(rects), N.ptr(keys[0]))
     N.check(lib.gs_project_forward(C.byref(pa), s), "gs_project_forward")
 
     fr = _Frame()
@@ -161,8 +161,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
                                         N.ptr(ws), ws.numel(), C.byref(alt), s), "depth sort")
         sorted_ids = vals[alt.value]
         bws = torch.empty((lib.gs_bin_workspace_bytes(n),), dtype=torch.uint8, device=dev)
-        ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(counters),
-                         N.ptr(bws), bws.numel(), 0, 0, 0)
+        ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(vis),
+                         N.ptr(counters), N.ptr(bws), bws.numel(), 0, 0, 0, N.ptr(records))
         StageTimer.mark("bin_count")
         N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
         StageTimer.mark("~sync")
@@ -182,10 +182,9 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
 
     num_tiles = cam.tiles_x * cam.tiles_y
     tk = torch.empty((2, T), dtype=i32, device=dev)
-    tv = torch.empty((2, T), dtype=i32, device=dev)
-    pair_gauss = torch.empty((T,), dtype=i32, device=dev)
+    tv = torch.empty((2, T), dtype=i32, device=dev)  # values = Gaussian ids
     pair_offset = torch.empty((n,), dtype=i32, device=dev)
-    ba.tile_keys, ba.pair_gauss, ba.pair_offset = N.ptr(tk[0]), N.ptr(pair_gauss), N.ptr(pair_offset)
+    ba.tile_keys, ba.pair_gauss, ba.pair_offset = N.ptr(tk[0]), N.ptr(tv[0]), N.ptr(pair_offset)
     StageTimer.mark("bin_emit")
     N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
 
@@ -193,13 +192,11 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     tws = torch.empty((lib.gs_radix_sort_workspace_bytes(T),), dtype=torch.uint8, device=dev)
     alt = C.c_int32(0)
     StageTimer.mark("tile_sort")
-    N.check(lib.gs_radix_sort_pairs(N.ptr(tk[0]), N.ptr(tv[0]), N.ptr(tk[1]), N.ptr(tv[1]), T, 0, bits, 1,
+    N.check(lib.gs_radix_sort_pairs(N.ptr(tk[0]), N.ptr(tv[0]), N.ptr(tk[1]), N.ptr(tv[1]), T, 0, bits, 0,
                                     N.ptr(tws), tws.numel(), C.byref(alt), s), "tile sort")
-    sorted_keys, sorted_pairs = tk[alt.value], tv[alt.value]
+    sorted_keys, sorted_gauss = tk[alt.value], tv[alt.value]
     ranges = torch.empty((num_tiles, 2), dtype=i32, device=dev)
-    sorted_gauss = torch.empty((T,), dtype=i32, device=dev)
-    ra = N.GsRangeArgs(T, num_tiles, N.ptr(sorted_keys), N.ptr(sorted_pairs), N.ptr(pair_gauss), N.ptr(ranges),
-                       N.ptr(sorted_gauss))
+    ra = N.GsRangeArgs(T, num_tiles, N.ptr(sorted_keys), N.ptr(ranges))
     StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
@@ -214,7 +211,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
     StageTimer.mark("~end_fwd")
 
-    fr.pair_offset, fr.ranges, fr.sorted_gauss, fr.sorted_pairs = pair_offset, ranges, sorted_gauss, sorted_pairs
+    fr.pair_offset, fr.ranges, fr.sorted_gauss = pair_offset, ranges, sorted_gauss
     fr.pix_acc, fr.pix_state = pix_acc, pix_state
     return image, alpha, depth, means2d, conics, radii, vis, fr
 
@@ -237,7 +234,7 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_depth = None if g_depth is None else g_depth.contiguous()
         pair_grads = torch.empty((max(fr.T, 1), N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
-                              N.ptr(fr.sorted_pairs), N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
+                              N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(pair_grads))
         StageTimer.mark("blend_bwd")
         N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
