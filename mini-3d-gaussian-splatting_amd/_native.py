@@ -17,7 +17,8 @@ import torch  # noqa: F401  (must be loaded before the HIP library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libgsplat_mi355x.so"
-LIB_PATH = os.path.join(_HERE, LIB_NAME)
+# GS_LIB_PATH overrides the in-tree library (A/B runs of kernel variants)
+LIB_PATH = os.environ.get("GS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 
 GS_TILE = 16
 GS_RECORD_FLOATS = 12

@@ -27,7 +27,7 @@ constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
 constexpr int kSortIpt = 8;                      // items per thread per sort block
 constexpr int kSortChunk = kBlock * kSortIpt;    // 2048 items per block
-constexpr int kBinChunk = kBlock * 16;           // 4096 Gaussians per binning block
+constexpr int kBinChunk = kBlock * 4;            // 1024 Gaussians per binning block
 constexpr float kAlphaStop = 0.995f;             // renderer.py:352
 constexpr float kMinWeight = 1e-5f;              // renderer.py:336
 
@@ -53,6 +53,19 @@ inline unsigned div_up(long long a, long long b) { return (unsigned)((a + b - 1)
 __device__ __forceinline__ float clamp01(float v) { return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
 __device__ __forceinline__ float clampf(float v, float lo, float hi) {
   return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// expf for x in [-87, 88]: the same instruction sequence as ocml's expf
+// (Cody-Waite split of x*log2(e), v_exp_f32, ldexp) without its overflow /
+// underflow selects, which the blend never reaches (it only evaluates
+// exp(-s/2) for s <= 23.1).  Bit-identical to expf on that range.
+__device__ __forceinline__ float exp_inrange(float x) {
+  const float ph = x * 0x1.715476p+0f;
+  float pl = __builtin_fmaf(x, 0x1.715476p+0f, -ph);
+  pl = __builtin_fmaf(x, 0x1.4ae0bep-26f, pl);
+  const float e = __builtin_rintf(ph);
+  const float a = (ph - e) + pl;
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(a), (int)e);
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -465,20 +478,22 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
       s_r2[threadIdx.x] = recs[3 * (size_t)gid + 2];
     }
     __syncthreads();
-    if (!done) {
+    // Control flow stays wave-uniform (ballots); per-lane decisions are
+    // predicates, and a skipped pair adds exact zeros.
+    if (__ballot(!done)) {
       for (uint32_t j = 0; j < cnt; ++j) {
         const float4 r0 = s_r0[j];
         const float4 r1 = s_r1[j];
         const float dx = fx - r0.x, dy = fy - r0.y;
         const float s = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;  // :333
-        // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp;
-        // the branch is taken by the whole wave or the exp is predicated.
-        if (!(s > 23.1f)) {
-          const float w = clamp01(expf(-0.5f * s));  // :334
-          const float ai = clamp01(r1.y * w);        // :339
-          const float c0 = (1.f - A) * ai;           // :343-344
-          // :336 / :340 / :345 skips as a predicate; a skipped pair adds exact zeros
-          const bool take = !(w < kMinWeight) && !(ai <= 0.f) && !(c0 <= 0.f);
+        // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp
+        const bool live = !done && !(s > 23.1f);
+        if (__ballot(live)) {
+          const float w = clamp01(exp_inrange(-0.5f * s));  // :334
+          const float ai = clamp01(r1.y * w);                // :339
+          const float c0 = (1.f - A) * ai;                   // :343-344
+          // :336 / :340 / :345 skips
+          const bool take = live && !(w < kMinWeight) && !(ai <= 0.f) && !(c0 <= 0.f);
           const float c = take ? c0 : 0.f;
           const float4 r2 = s_r2[j];
           ar += c * r2.x;
@@ -486,11 +501,10 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
           ab += c * r2.z;
           A = A + c;
           D += c * r1.z;
-          if (take && A >= kAlphaStop) {  // :352 (after accumulation)
-            done = true;
-            neval = b - start + j + 1;
-            break;
-          }
+          const bool term = take && A >= kAlphaStop;  // :352 (after accumulation)
+          neval = term ? b - start + j + 1 : neval;
+          done = done || term;
+          if (!__ballot(!done)) break;
         }
       }
     }
@@ -610,36 +624,32 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
     const uint32_t jbase = b - start;
     for (uint32_t j = 0; j < cnt; ++j) {
       float dop = 0.f, cw = 0.f;
-      if (jbase + j < neval) {
-        const float4 r0 = s_r0[j];
-        const float4 r1 = s_r1[j];
-        const float dx = fx - r0.x, dy = fy - r0.y;
-        const float sq = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;
-        if (!(sq > 23.1f)) {  // exp(-11.55) < 1e-5: exact early skip (NaN falls through)
-          const float e = expf(-0.5f * sq);
-          const float w = clamp01(e);
-          const float u = r1.y * w;
-          const float ai = clamp01(u);
-          const float trans = 1.f - A;
-          const float c = trans * ai;
-          if (!(w < kMinWeight) && !(ai <= 0.f) && !(c <= 0.f)) {  // the forward's three skips, NaN-exact
-            const float4 r2 = s_r2[j];
-            const float X = __builtin_fmaf(gR0, r2.x, __builtin_fmaf(gR1, r2.y, __builtin_fmaf(gR2, r2.z, gD * r1.z)));
-            A = A + c;
-            float dal;
-            if (A >= kAlphaStop) {
-              // the terminating contributor: nothing behind it, (1-A_total)/T_{i+1} = 1
-              dal = trans * (X + gA);
-            } else {
-              P = __builtin_fmaf(c, X, P);
-              const float inv = __frcp_rn(1.f - A);
-              dal = trans * __builtin_fmaf(inv, __builtin_fmaf(gA, onemA, P - K), X);
-            }
-            const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
-            dop = du * w;
-            cw = (e >= 0.f && e <= 1.f) ? c : -c;
-          }
-        }
+      const float4 r0 = s_r0[j];
+      const float4 r1 = s_r1[j];
+      const float dx = fx - r0.x, dy = fy - r0.y;
+      const float sq = ((dx * dx) * r0.z + (r0.w * dx) * dy) + (dy * dy) * r1.x;
+      // exp(-11.55) < 1e-5: exact early skip (NaN falls through), as in the forward
+      const bool live = (jbase + j < neval) && !(sq > 23.1f);
+      if (__ballot(live)) {
+        const float e = exp_inrange(-0.5f * sq);
+        const float w = clamp01(e);
+        const float u = r1.y * w;
+        const float ai = clamp01(u);
+        const float trans = 1.f - A;
+        const float c0 = trans * ai;
+        const bool take = live && !(w < kMinWeight) && !(ai <= 0.f) && !(c0 <= 0.f);  // the forward's skips
+        const float c = take ? c0 : 0.f;
+        const float4 r2 = s_r2[j];
+        const float X = __builtin_fmaf(gR0, r2.x, __builtin_fmaf(gR1, r2.y, __builtin_fmaf(gR2, r2.z, gD * r1.z)));
+        A = A + c;
+        P = __builtin_fmaf(c, X, P);
+        // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
+        const bool term = A >= kAlphaStop;
+        const float inv = __frcp_rn(1.f - A);
+        const float dal = trans * (term ? X + gA : __builtin_fmaf(inv, __builtin_fmaf(gA, onemA, P - K), X));
+        const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
+        dop = take ? du * w : 0.f;
+        cw = take ? ((e >= 0.f && e <= 1.f) ? c : -c) : 0.f;
       }
       s_dop[j][tid] = dop;
       s_c[j][tid] = cw;
