@@ -104,10 +104,10 @@ def main():
     scene = pkg.synthetic.make_scene(n, W, H, seed=0)
     model = pkg.synthetic.to_model(scene, pkg.GaussianModel, dev)
     params = model.grad_parameters()
-    opt = None if a.no_optimizer else torch.optim.Adam(
+    opt = None if a.no_optimizer else pkg.optim.FusedAdam(
         [{"params": [model._xyz], "lr": 1.6e-4}, {"params": [model._features_dc], "lr": 2.5e-3},
          {"params": [model._opacity], "lr": 0.05}, {"params": [model._scaling], "lr": 5e-3},
-         {"params": [model._rotation], "lr": 1e-3}], fused=True)
+         {"params": [model._rotation], "lr": 1e-3}])
     cam = BenchCamera(W, H, scene.fovx, scene.fovy, view_matrix(rank))
     settings = pkg.RenderSettings(image_height=H, image_width=W, bg_color=torch.zeros(3))
     renderer = pkg.GaussianRenderer()

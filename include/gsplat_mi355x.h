@@ -208,6 +208,8 @@ typedef struct gs_project_bwd_args {
   const uint8_t *vis;
   const uint32_t *rects;
   const uint32_t *pair_offset;
+  const uint32_t *order;       /* [n] permutation to walk the Gaussians in (the depth-sorted
+                                  ids: their slot ranges are then adjacent, reads coalesce); or NULL */
   const float *pair_grads;     /* may be NULL when T == 0 */
   const float *g_means2d;      /* [n,2] or NULL */
   const float *g_conics;       /* [n,4] or NULL */
@@ -219,6 +221,29 @@ typedef struct gs_project_bwd_args {
   float *d_opacity;            /* [n]   */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
+
+/* ---- Adam step over several parameter tensors, one launch -----------------
+ * SURVEY 8(f) row 1 (fused Adam), the optimizer the reference builds in
+ * src/core/optimizer.py:100-113 (torch.optim.Adam, 5 parameter groups).
+ * torch.optim.Adam semantics (amsgrad off, weight_decay 0):
+ *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
+ *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+ * Tensors with grad == NULL are skipped (torch skips params without grad). */
+#define GS_ADAM_MAX_TENSORS 8
+typedef struct gs_adam_tensor {
+  float *param, *exp_avg, *exp_avg_sq;
+  const float *grad;     /* NULL: skip */
+  int64_t numel;
+  float lr;
+  float bias_correction1; /* 1 - beta1^step */
+  float bias_correction2_sqrt; /* sqrt(1 - beta2^step) */
+} gs_adam_tensor;
+typedef struct gs_adam_args {
+  int32_t num_tensors;
+  float beta1, beta2, eps;
+  gs_adam_tensor t[GS_ADAM_MAX_TENSORS];
+} gs_adam_args;
+gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream);
 
 /* ---- misc --------------------------------------------------------------- */
 int32_t gs_abi_version(void);

@@ -87,9 +87,26 @@ class GsBlendBwdArgs(C.Structure):
 class GsProjectBwdArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("g", GsGaussians), ("means2d", _vp), ("conics", _vp), ("vis", _vp),
-        ("rects", _vp), ("pair_offset", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
+        ("rects", _vp), ("pair_offset", _vp), ("order", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
         ("g_conics", _vp), ("d_xyz", _vp), ("d_cov3d", _vp), ("d_scaling", _vp),
         ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp),
+    ]
+
+
+GS_ADAM_MAX_TENSORS = 8
+
+
+class GsAdamTensor(C.Structure):
+    _fields_ = [
+        ("param", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("grad", _vp), ("numel", C.c_int64),
+        ("lr", C.c_float), ("bias_correction1", C.c_float), ("bias_correction2_sqrt", C.c_float),
+    ]
+
+
+class GsAdamArgs(C.Structure):
+    _fields_ = [
+        ("num_tensors", C.c_int32), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+        ("t", GsAdamTensor * GS_ADAM_MAX_TENSORS),
     ]
 
 
@@ -97,7 +114,7 @@ class GsProjectBwdArgs(C.Structure):
 EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
-    "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
+    "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward", "gs_adam_step",
 )
 
 _lib = None
@@ -125,8 +142,10 @@ def _declare(lib):
     lib.gs_blend_forward.argtypes = [P(GsBlendFwdArgs), _vp]
     lib.gs_blend_backward.argtypes = [P(GsBlendBwdArgs), _vp]
     lib.gs_project_backward.argtypes = [P(GsProjectBwdArgs), _vp]
+    lib.gs_adam_step.argtypes = [P(GsAdamArgs), _vp]
     for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_bin_count", "gs_bin_emit",
-              "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward"):
+              "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
+              "gs_adam_step"):
         getattr(lib, f).restype = C.c_int
 
 

@@ -534,7 +534,11 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
 //  B (entry-parallel): each 16-lane row owns one entry, sums its 256 pixels
 //    (16 per lane) into the 10 gradient values, reduces the row with DPP and
 //    writes the entry's slot.
-constexpr int kBwdBatch = 16;
+#ifndef GS_BWD_BATCH
+#define GS_BWD_BATCH 16
+#endif
+constexpr int kBwdBatch = GS_BWD_BATCH;        // entries per batch: 8 or 16
+constexpr int kRowsPerEntry = 16 / kBwdBatch;  // 16-lane DPP rows summing one entry
 constexpr int kPdStride = kBlock + 16;  // rows of the pair arrays: +16 floats keeps 16-lane rows on disjoint banks
 
 template <int CTRL>
@@ -603,7 +607,8 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   float P = (gR0 * bg0 + gR1 * bg1) + gR2 * bg2;
   float A = 0.f;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
-  const int jj = tid >> 4, sub = tid & 15;  // phase B: row jj owns entry jj
+  // phase B: 16-lane row r = tid >> 4 works on entry r / kRowsPerEntry, pixel groups k = part (mod kRowsPerEntry)
+  const int jj = (tid >> 4) / kRowsPerEntry, part = (tid >> 4) % kRowsPerEntry, sub = tid & 15;
   for (uint32_t b = start; b < stop; b += kBwdBatch) {
     const uint32_t cnt = min((uint32_t)kBwdBatch, stop - b);
     __syncthreads();  // previous phase B done with s_r*, s_dop, s_c
@@ -666,7 +671,8 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy) with Sx = sum ds dx, Sy = sum ds dy
       float Sx = 0.f, Sy = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
 #pragma unroll
-      for (int k = 0; k < kBlock / 16; ++k) {
+      for (int kk = 0; kk < 16 / kRowsPerEntry; ++kk) {
+        const int k = part + kRowsPerEntry * kk;
         const int p = sub + 16 * k;
         const float dop = s_dop[jj][p], cs = s_c[jj][p];
         const float4 pg = s_pg[p];
@@ -687,7 +693,12 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       }
       Sx = row16_sum(Sx); Sy = row16_sum(Sy); g2 = row16_sum(g2); g3 = row16_sum(g3); g4 = row16_sum(g4);
       g5 = row16_sum(g5); g6 = row16_sum(g6); g7 = row16_sum(g7); g8 = row16_sum(g8); g9 = row16_sum(g9);
-      if (sub == 0) {
+      if (kRowsPerEntry == 2) {  // rows 2i, 2i+1 of a wave hold halves of one entry
+        Sx += __shfl_xor(Sx, 16); Sy += __shfl_xor(Sy, 16); g2 += __shfl_xor(g2, 16); g3 += __shfl_xor(g3, 16);
+        g4 += __shfl_xor(g4, 16); g5 += __shfl_xor(g5, 16); g6 += __shfl_xor(g6, 16); g7 += __shfl_xor(g7, 16);
+        g8 += __shfl_xor(g8, 16); g9 += __shfl_xor(g9, 16);
+      }
+      if (sub == 0 && part == 0) {
         const float q00 = r0.z, qo = r0.w, q11 = r1.x;
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
         float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)s_e[jj] * GS_PAIR_GRAD_FLOATS);
@@ -714,8 +725,10 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
 
 // ======================================================== project bwd =====
 __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
-  const int g = blockIdx.x * kBlock + threadIdx.x;
-  if (g >= a.g.n) return;
+  const int k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= a.g.n) return;
+  // in depth order, consecutive threads own adjacent slot ranges
+  const int g = a.order ? (int)a.order[k] : k;
   float acc[GS_PAIR_GRAD_FLOATS];
 #pragma unroll
   for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
@@ -898,6 +911,55 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
 }
 
 // tile coordinates are packed in 12 bits (record word 11): images up to 65536 px a side
+
+// ======================================================== Adam ============
+// One launch for all tensors: block b -> (tensor, chunk of kAdamChunk floats)
+// through a prefix table in the kernel arguments; float4 streaming.
+constexpr int kAdamChunk = kBlock * 4 * 4;  // 4096 floats per block
+
+__global__ __launch_bounds__(kBlock) void k_adam(gs_adam_args a, int4 firsts0, int4 firsts1) {
+  const int starts[GS_ADAM_MAX_TENSORS + 1] = {firsts0.x, firsts0.y, firsts0.z, firsts0.w,
+                                               firsts1.x, firsts1.y, firsts1.z, firsts1.w, 0x7fffffff};
+  int ti = 0;
+#pragma unroll
+  for (int k = 1; k < GS_ADAM_MAX_TENSORS; ++k) ti += (int)blockIdx.x >= starts[k] ? 1 : 0;
+  const gs_adam_tensor &t = a.t[ti];
+  if (!t.grad) return;
+  const int64_t base = (int64_t)(blockIdx.x - starts[ti]) * kAdamChunk;
+  const float b1 = a.beta1, b2 = a.beta2, om1 = 1.f - b1, om2 = 1.f - b2;
+  const float step = t.lr / t.bias_correction1, bc2s = t.bias_correction2_sqrt;
+  const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
+                     reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
+  for (int r = 0; r < 4; ++r) {
+    const int64_t i0 = base + ((int64_t)r * kBlock + threadIdx.x) * 4;
+    if (i0 >= t.numel) break;
+    if (vec && i0 + 4 <= t.numel) {
+      float4 p = *reinterpret_cast<const float4 *>(t.param + i0);
+      const float4 g = *reinterpret_cast<const float4 *>(t.grad + i0);
+      float4 m = *reinterpret_cast<const float4 *>(t.exp_avg + i0);
+      float4 v = *reinterpret_cast<const float4 *>(t.exp_avg_sq + i0);
+#define GS_ADAM_1(c)                                              \
+      m.c = m.c + om1 * (g.c - m.c);                              \
+      v.c = b2 * v.c + om2 * (g.c * g.c);                         \
+      p.c -= step * (m.c / (sqrtf(v.c) / bc2s + a.eps));
+      GS_ADAM_1(x) GS_ADAM_1(y) GS_ADAM_1(z) GS_ADAM_1(w)
+#undef GS_ADAM_1
+      *reinterpret_cast<float4 *>(t.param + i0) = p;
+      *reinterpret_cast<float4 *>(t.exp_avg + i0) = m;
+      *reinterpret_cast<float4 *>(t.exp_avg_sq + i0) = v;
+    } else {
+      for (int64_t i = i0; i < i0 + 4 && i < t.numel; ++i) {
+        const float g = t.grad[i];
+        const float m = t.exp_avg[i] + om1 * (g - t.exp_avg[i]);
+        const float v = b2 * t.exp_avg_sq[i] + om2 * (g * g);
+        t.exp_avg[i] = m;
+        t.exp_avg_sq[i] = v;
+        t.param[i] -= step * (m / (sqrtf(v) / bc2s + a.eps));
+      }
+    }
+  }
+}
+
 bool cam_ok(const gs_camera &c) {
   return c.tile_size == GS_TILE && c.image_width > 0 && c.image_height > 0 &&
          c.image_width <= (GS_TILE << 12) && c.image_height <= (GS_TILE << 12);
@@ -1043,6 +1105,30 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   hipStream_t s = (hipStream_t)stream;
   k_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_backward");
+}
+
+gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream) {
+  if (!a || a->num_tensors < 0 || a->num_tensors > GS_ADAM_MAX_TENSORS)
+    return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_adam_step");
+  int starts[GS_ADAM_MAX_TENSORS] = {0};
+  long long nblk = 0;
+  for (int i = 0; i < GS_ADAM_MAX_TENSORS; ++i) {
+    starts[i] = (int)nblk;
+    if (i < a->num_tensors) {
+      const gs_adam_tensor &t = a->t[i];
+      if (t.grad && (!t.param || !t.exp_avg || !t.exp_avg_sq || t.numel < 0))
+        return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_adam_step");
+      nblk += t.grad ? (t.numel + kAdamChunk - 1) / kAdamChunk : 0;
+    }
+  }
+  if (nblk == 0) return GS_OK;
+  if (nblk > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many elements", "gs_adam_step");
+  // tensors without grad get no blocks: zero-length ranges in the table
+  gs_adam_args c = *a;
+  for (int i = a->num_tensors; i < GS_ADAM_MAX_TENSORS; ++i) c.t[i].grad = nullptr;
+  k_adam<<<(unsigned)nblk, kBlock, 0, (hipStream_t)stream>>>(
+      c, make_int4(starts[0], starts[1], starts[2], starts[3]), make_int4(starts[4], starts[5], starts[6], starts[7]));
+  return check_launch("gs_adam_step");
 }
 
 }  // extern "C"

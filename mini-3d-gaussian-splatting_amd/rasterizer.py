@@ -122,8 +122,8 @@ def _check_inputs(xyz: torch.Tensor):
 
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
-    __slots__ = ("records", "rects", "vis", "pair_offset", "ranges", "sorted_gauss", "pix_acc", "pix_state",
-                 "M", "T")
+    __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_acc",
+                 "pix_state", "M", "T")
 
 
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity):
@@ -152,7 +152,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     N.check(lib.gs_project_forward(C.byref(pa), s), "gs_project_forward")
 
     fr = _Frame()
-    fr.records, fr.rects, fr.vis = records, rects, vis
+    fr.records, fr.rects, fr.vis, fr.order = records, rects, vis, None
     if n > 0:
         ws = torch.empty((lib.gs_radix_sort_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         StageTimer.mark("depth_sort")
@@ -160,6 +160,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         N.check(lib.gs_radix_sort_pairs(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n, 0, 32, 1,
                                         N.ptr(ws), ws.numel(), C.byref(alt), s), "depth sort")
         sorted_ids = vals[alt.value]
+        fr.order = sorted_ids
         bws = torch.empty((lib.gs_bin_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(vis),
                          N.ptr(counters), N.ptr(bws), bws.numel(), 0, 0, 0, N.ptr(records))
@@ -249,7 +250,9 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     gc = None if g_conics is None else g_conics.contiguous()
     gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity)
     pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
-                            N.ptr(fr.pair_offset), N.ptr(pair_grads), N.ptr(gm), N.ptr(gc), N.ptr(d_xyz),
+                            # Gaussian order (order=NULL): inputs/outputs stream; walking in depth
+                            # order coalesces the slot reads but scatters 10 arrays (measured 2.4x slower)
+                            N.ptr(fr.pair_offset), None, N.ptr(pair_grads), N.ptr(gm), N.ptr(gc), N.ptr(d_xyz),
                             N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op))
     StageTimer.mark("project_bwd")
     N.check(lib.gs_project_backward(C.byref(pb), s), "gs_project_backward")

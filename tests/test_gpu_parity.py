@@ -186,3 +186,26 @@ def test_deterministic(pkg, cuda):
         res.append((out["image"].clone(), m._xyz.grad.clone(), m._rotation.grad.clone()))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_fused_adam_matches_torch_adam(pkg, cuda):
+    """FusedAdam (one gs_adam_step launch) vs torch.optim.Adam, 5 groups as in
+    the reference's GaussianOptimizer (optimizer.py:100-113), one param without grad."""
+    g = torch.Generator().manual_seed(0)
+    shapes = [(1000, 3), (1000, 1, 3), (1000, 1), (1000, 3), (1000, 4), (1000, 15, 3)]
+    lrs = [1.6e-4, 2.5e-3, 0.05, 5e-3, 1e-3, 2.5e-3]
+    a = [torch.randn(s, generator=g).to(cuda).requires_grad_() for s in shapes]
+    b = [t.detach().clone().requires_grad_() for t in a]
+    oa = pkg.optim.FusedAdam([{"params": [t], "lr": lr} for t, lr in zip(a, lrs)])
+    ob = torch.optim.Adam([{"params": [t], "lr": lr} for t, lr in zip(b, lrs)])
+    for it in range(5):
+        for i, (x, y) in enumerate(zip(a, b)):
+            if i == 5:
+                x.grad = y.grad = None
+                continue
+            gr = torch.randn(shapes[i], generator=g).to(cuda)
+            x.grad, y.grad = gr.clone(), gr.clone()
+        oa.step()
+        ob.step()
+    for x, y in zip(a, b):
+        assert torch.allclose(x, y, rtol=1e-5, atol=1e-5), (x - y).abs().max()  # fp32 rounding of two Adam kernels
