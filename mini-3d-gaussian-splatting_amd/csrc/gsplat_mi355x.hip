@@ -51,6 +51,12 @@ inline unsigned div_up(long long a, long long b) { return (unsigned)((a + b - 1)
 
 // torch.clamp semantics (NaN propagates)
 __device__ __forceinline__ float clamp01(float v) { return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
+// clamp to [0,1] as the VALU clamp output modifier (folds into the producing
+// instruction).  Equals clamp01 for every non-NaN input; NaN -> 0 instead of
+// NaN (only reachable from NaN/inf inputs).  Used on the blend's hot path.
+__device__ __forceinline__ float sat01(float v) { return __builtin_amdgcn_fmed3f(v, 0.f, 1.f); }
+// wave-uniform "any lane" without the bool -> VGPR -> compare round trip
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 __device__ __forceinline__ float clampf(float v, float lo, float hi) {
   return v < lo ? lo : (v > hi ? hi : v);
 }
@@ -235,11 +241,11 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
       const float *cl = a.g.color_logits + (int64_t)g * a.g.color_stride;
       const float op = a.g.opacity[(int64_t)g * a.g.opacity_stride];
       float4 *rec = reinterpret_cast<float4 *>(a.records) + 3 * (int64_t)g;
-      // record: mx my q00 qo | q11 o z r | g b off rinfo  (read as 8-byte pairs by the blend)
+      // record: mx my q00 qo | q11 o r g | b z off rinfo  (read as 8-byte pairs by the blend)
       const float cr = 1.f / (1.f + expf(-cl[0])), cg = 1.f / (1.f + expf(-cl[1])), cb = 1.f / (1.f + expf(-cl[2]));  // sigmoid (:90)
       rec[0] = make_float4(mx, my, q0, q1 + q2);
-      rec[1] = make_float4(q3, op, Z, cr);
-      rec[2] = make_float4(cg, cb, 0.f, __uint_as_float(rinfo));
+      rec[1] = make_float4(q3, op, cr, cg);
+      rec[2] = make_float4(cb, Z, 0.f, __uint_as_float(rinfo));
     }
     reinterpret_cast<uint2 *>(a.rects)[g] = make_uint2(rx, ry);
     a.depth_keys[g] = visible ? __float_as_uint(Z) : 0xFFFFFFFFu;
@@ -457,7 +463,7 @@ __device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int &px, int &
 
 // Records staged in LDS are read as 8-byte pairs: ds_read_b64 costs 2 LDS
 // cycles per wave-instruction (broadcast), ds_read_b96 8 and ds_read_b128 4
-// (MI355X_MICROARCH.md, LDS table): (mx,my) (q00,qo) (q11,o) | (z,r) (g,b).
+// (MI355X_MICROARCH.md, LDS table): (mx,my) (q00,qo) (q11,o) | (r,g) (b,z).
 __device__ __forceinline__ float2 lds_pair(const float2 *p) {
   // volatile keeps each pair its own ds_read_b64 (no merging into b128 / read2)
   typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;
@@ -492,30 +498,30 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
     __syncthreads();
     // Control flow stays wave-uniform (ballots); per-lane decisions are
     // predicates, and a skipped pair adds exact zeros.
-    if (__ballot(!done)) {
+    if (wave_any(!done)) {
       for (uint32_t j = 0; j < cnt; ++j) {
         const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
         const float dx = fx - pm.x, dy = fy - pm.y;
         const float s = ((dx * dx) * pq.x + (pq.y * dx) * dy) + (dy * dy) * po.x;  // :333
         // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp
         const bool live = !done && !(s > 23.1f);
-        if (__ballot(live)) {
-          const float w = clamp01(exp_inrange(-0.5f * s));  // :334
-          const float ai = clamp01(po.y * w);                // :339
+        if (wave_any(live)) {
+          const float w = sat01(exp_inrange(-0.5f * s));  // :334
+          const float ai = sat01(po.y * w);                // :339
           const float c0 = (1.f - A) * ai;                   // :343-344
           // :336 / :340 / :345 skips
           const bool take = live && !(w < kMinWeight) && !(ai <= 0.f) && !(c0 <= 0.f);
           const float c = take ? c0 : 0.f;
-          const float2 pz = lds_pair(&s_rec[6 * j + 3]), pc = lds_pair(&s_rec[6 * j + 4]);
-          ar += c * pz.y;
-          ag += c * pc.x;
-          ab += c * pc.y;
+          const float2 prg = lds_pair(&s_rec[6 * j + 3]), pbz = lds_pair(&s_rec[6 * j + 4]);
+          ar += c * prg.x;
+          ag += c * prg.y;
+          ab += c * pbz.x;
           A = A + c;
-          D += c * pz.x;
+          D += c * pbz.y;
           const bool term = take && A >= kAlphaStop;  // :352 (after accumulation)
           neval = term ? b - start + j + 1 : neval;
           done = done || term;
-          if (!__ballot(!done)) break;
+          if (!wave_any(!done)) break;
         }
       }
     }
@@ -645,17 +651,17 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       const float sq = ((dx * dx) * pq.x + (pq.y * dx) * dy) + (dy * dy) * po.x;
       // exp(-11.55) < 1e-5: exact early skip (NaN falls through), as in the forward
       const bool live = (jbase + j < neval) && !(sq > 23.1f);
-      if (__ballot(live)) {
+      if (wave_any(live)) {
         const float e = exp_inrange(-0.5f * sq);
-        const float w = clamp01(e);
+        const float w = sat01(e);
         const float u = po.y * w;
-        const float ai = clamp01(u);
+        const float ai = sat01(u);
         const float trans = 1.f - A;
         const float c0 = trans * ai;
         const bool take = live && !(w < kMinWeight) && !(ai <= 0.f) && !(c0 <= 0.f);  // the forward's skips
         const float c = take ? c0 : 0.f;
-        const float2 pz = lds_pair(&s_rec[6 * j + 3]), pc = lds_pair(&s_rec[6 * j + 4]);
-        const float X = __builtin_fmaf(gR0, pz.y, __builtin_fmaf(gR1, pc.x, __builtin_fmaf(gR2, pc.y, gD * pz.x)));
+        const float2 prg = lds_pair(&s_rec[6 * j + 3]), pbz = lds_pair(&s_rec[6 * j + 4]);
+        const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
         A = A + c;
         P = __builtin_fmaf(c, X, P);
         // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
