@@ -300,6 +300,9 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
                                                           int nbits, const uint32_t *counts,
                                                           const uint32_t *totals, int nb) {
   __shared__ uint32_t wcnt[4][kRadix];
+  __shared__ uint32_t s_lbase[kRadix];  // block-local start of each digit
+  __shared__ uint32_t s_gbase[kRadix];  // global start of this block's run of each digit
+  __shared__ uint32_t s_k[kSortChunk], s_v[kSortChunk];
   __shared__ uint32_t s_tmp[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -307,7 +310,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
   uint32_t tot;
   const uint32_t dbase = block_exscan(totals[threadIdx.x], s_tmp, &tot);  // includes a barrier
   const uint32_t mask = (1u << nbits) - 1u;
-  const long long base = (long long)blockIdx.x * kSortChunk + wave * (kSortChunk / 4);
+  const long long blk0 = (long long)blockIdx.x * kSortChunk;
+  const long long base = blk0 + wave * (kSortChunk / 4);
   uint32_t k_[kSortIpt], v_[kSortIpt], rk[kSortIpt];
 #pragma unroll
   for (int r = 0; r < kSortIpt; ++r) {
@@ -327,23 +331,39 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
   }
   __syncthreads();
   {
-    uint32_t run = dbase + counts[(size_t)threadIdx.x * nb + blockIdx.x];
+    // per digit: wave prefixes inside the block, block count, then the
+    // block-local digit start (scan over digits)
+    uint32_t run = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const uint32_t t = wcnt[w][threadIdx.x];
       wcnt[w][threadIdx.x] = run;
       run += t;
     }
+    const uint32_t lb = block_exscan(run, s_tmp, &tot);  // barrier inside
+    s_lbase[threadIdx.x] = lb;
+    s_gbase[threadIdx.x] = dbase + counts[(size_t)threadIdx.x * nb + blockIdx.x];
   }
   __syncthreads();
+  // locally sorted chunk in LDS (stable: wave, round, lane order within a digit)
 #pragma unroll
   for (int r = 0; r < kSortIpt; ++r) {
     if (rk[r] != 0xFFFFFFFFu) {
       const uint32_t d = (k_[r] >> shift) & mask;
-      const uint32_t dst = wcnt[wave][d] + rk[r];
-      keys_out[dst] = k_[r];
-      vals_out[dst] = v_[r];
+      const uint32_t lp = s_lbase[d] + wcnt[wave][d] + rk[r];
+      s_k[lp] = k_[r];
+      s_v[lp] = v_[r];
     }
+  }
+  __syncthreads();
+  // write out: consecutive threads -> consecutive positions of one digit run
+  const int cnt = (int)min((long long)kSortChunk, (long long)n - blk0);
+  for (int i = threadIdx.x; i < cnt; i += kBlock) {
+    const uint32_t key = s_k[i];
+    const uint32_t d = (key >> shift) & mask;
+    const uint32_t dst = s_gbase[d] + (uint32_t)i - s_lbase[d];
+    keys_out[dst] = key;
+    vals_out[dst] = s_v[i];
   }
 }
 
