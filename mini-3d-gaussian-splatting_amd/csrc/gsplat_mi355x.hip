@@ -55,6 +55,11 @@ __device__ __forceinline__ float clamp01(float v) { return v < 0.f ? 0.f : (v > 
 // instruction).  Equals clamp01 for every non-NaN input; NaN -> 0 instead of
 // NaN (only reachable from NaN/inf inputs).  Used on the blend's hot path.
 __device__ __forceinline__ float sat01(float v) { return __builtin_amdgcn_fmed3f(v, 0.f, 1.f); }
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt) but NOT for its global loads, unlike __syncthreads() whose
+// workgroup fence drains vmcnt -- prefetched gathers stay in flight across it.
+// The "memory" clobber keeps the compiler from moving memory ops across.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // wave-uniform "any lane" without the bool -> VGPR -> compare round trip
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 __device__ __forceinline__ float clampf(float v, float lo, float hi) {
@@ -506,16 +511,30 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
   uint32_t neval = 0;
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
+  __shared__ uint32_t s_live[4];
+  // batch i+1's records are gathered into registers while batch i composites
+  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
+  if (start + threadIdx.x < end) {
+    const uint32_t gid = a.sorted_gauss[start + threadIdx.x];
+    n0 = recs[3 * (size_t)gid];
+    n1 = recs[3 * (size_t)gid + 1];
+    n2 = recs[3 * (size_t)gid + 2];
+  }
   for (uint32_t b = start; b < end; b += kBlock) {
     const uint32_t cnt = min((uint32_t)kBlock, end - b);
-    if (threadIdx.x < cnt) {
-      const uint32_t gid = a.sorted_gauss[b + threadIdx.x];
+    {  // (the previous round ended in a barrier after its last LDS read)
       float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * threadIdx.x]);
-      d[0] = recs[3 * (size_t)gid];
-      d[1] = recs[3 * (size_t)gid + 1];
-      d[2] = recs[3 * (size_t)gid + 2];
+      d[0] = n0;
+      d[1] = n1;
+      d[2] = n2;
     }
-    __syncthreads();
+    lds_barrier();
+    if (b + kBlock + threadIdx.x < end) {
+      const uint32_t gid = a.sorted_gauss[b + kBlock + threadIdx.x];
+      n0 = recs[3 * (size_t)gid];
+      n1 = recs[3 * (size_t)gid + 1];
+      n2 = recs[3 * (size_t)gid + 2];
+    }
     // Control flow stays wave-uniform (ballots); per-lane decisions are
     // predicates, and a skipped pair adds exact zeros.
     if (wave_any(!done)) {
@@ -545,7 +564,14 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         }
       }
     }
-    if (__syncthreads_count(done) == kBlock) break;
+    // all pixels of the tile done? (per-wave ballot -- taken with every lane
+    // active, outside the lane-0 branch -- then the 4 wave flags)
+    const bool wave_live = wave_any(!done);
+    if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = wave_live ? 1u : 0u;
+    lds_barrier();
+    const uint32_t any_live = s_live[0] | s_live[1] | s_live[2] | s_live[3];
+    lds_barrier();  // s_live / s_rec reads done before the next round writes them
+    if (!any_live) break;
   }
   if (!inside) return;
   if (!done) neval = end - start;
@@ -646,22 +672,36 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   // phase B: 16-lane row r = tid >> 4 works on entry r / kRowsPerEntry, pixel groups k = part (mod kRowsPerEntry)
   const int jj = (tid >> 4) / kRowsPerEntry, part = (tid >> 4) % kRowsPerEntry, sub = tid & 15;
+  // batch i+1's records are gathered into registers (threads < kBwdBatch)
+  // while batch i is processed; lds_barrier() keeps those loads in flight
+  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
+  if (tid < kBwdBatch && start + tid < stop) {
+    const uint32_t gid = a.sorted_gauss[start + tid];
+    n0 = recs[3 * (size_t)gid];
+    n1 = recs[3 * (size_t)gid + 1];
+    n2 = recs[3 * (size_t)gid + 2];
+  }
+  const uint32_t tile_x = (uint32_t)(tile % a.tiles_x), tile_y = (uint32_t)(tile / a.tiles_x);
   for (uint32_t b = start; b < stop; b += kBwdBatch) {
     const uint32_t cnt = min((uint32_t)kBwdBatch, stop - b);
-    __syncthreads();  // previous phase B done with s_r*, s_dop, s_c
-    if (tid < cnt) {
-      const uint32_t gid = a.sorted_gauss[b + tid];
-      const float4 r2 = recs[3 * (size_t)gid + 2];
+    lds_barrier();  // previous phase B done with s_rec, s_e, s_dop, s_c
+    if (tid < kBwdBatch) {
       float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * tid]);
-      d[0] = recs[3 * (size_t)gid];
-      d[1] = recs[3 * (size_t)gid + 1];
-      d[2] = r2;
+      d[0] = n0;
+      d[1] = n1;
+      d[2] = n2;
       // emit index of this entry: pair_offset[g] + the tile's index in g's rectangle
-      const uint32_t info = __float_as_uint(r2.w);
-      const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
-      s_e[tid] = __float_as_uint(r2.z) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) + (tx - (info & 0xFFFu));
+      const uint32_t info = __float_as_uint(n2.w);
+      s_e[tid] = __float_as_uint(n2.z) + (tile_y - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
+                 (tile_x - (info & 0xFFFu));
+      if (b + kBwdBatch + tid < stop) {
+        const uint32_t gid = a.sorted_gauss[b + kBwdBatch + tid];
+        n0 = recs[3 * (size_t)gid];
+        n1 = recs[3 * (size_t)gid + 1];
+        n2 = recs[3 * (size_t)gid + 2];
+      }
     }
-    __syncthreads();
+    lds_barrier();
     // ---- phase A: replay ------------------------------------------------
     const uint32_t jbase = b - start;
     for (uint32_t j = 0; j < cnt; ++j) {
@@ -695,7 +735,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       s_dop[j][tid] = dop;
       s_c[j][tid] = cw;
     }
-    __syncthreads();
+    lds_barrier();
     // ---- phase B: per-entry sums ----------------------------------------
     if ((uint32_t)jj < cnt) {
       const float2 pm = s_rec[6 * jj], pq = s_rec[6 * jj + 1], po = s_rec[6 * jj + 2];

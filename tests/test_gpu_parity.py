@@ -209,3 +209,29 @@ def test_fused_adam_matches_torch_adam(pkg, cuda):
         ob.step()
     for x, y in zip(a, b):
         assert torch.allclose(x, y, rtol=1e-5, atol=1e-5), (x - y).abs().max()  # fp32 rounding of two Adam kernels
+
+
+@pytest.mark.parametrize("bg", [(0.0, 0.0, 0.0), (0.3, 0.2, 0.1)])
+def test_long_tile_lists_vs_oracle(pkg, cuda, bg):
+    """Tiles with > 256 entries (several forward batches, many backward
+    batches) and low opacities, so pixels run deep into their lists."""
+    syn = pkg.synthetic
+    n, w, h = 20000, 48, 40
+    sc = syn.make_scene(n, w, h, seed=7, sigma_range=(0.05, 0.15), z_range=(3.0, 4.0))
+    sc.opacity.fill_(-2.5)  # sigmoid ~ 0.08: ~90% of pixels terminate, thousands of entries deep
+    m = syn.to_model(sc, pkg.GaussianModel, cuda)
+    out = pkg.GaussianRenderer().render(Cam(w, h, sc.fovx, sc.fovy), m, pkg.RenderSettings(h, w, torch.tensor(bg)))
+    rng = np.random.default_rng(2)
+    gi, ga, gd = (rng.uniform(-1, 1, s).astype(np.float32) for s in ((3, h, w), (1, h, w), (1, h, w)))
+    L = sum((out[k] * torch.tensor(v, device=cuda)).sum() for k, v in (("image", gi), ("alpha", ga), ("depth", gd)))
+    L.backward()
+    cov = G.oracle().covariance(sc.scaling.numpy(), sc.rotation.numpy())
+    ref = G.oracle().render_backward(_oracle_scene(sc, cov, bg), gi, ga, gd)
+    assert ref["T"] / ((w + 15) // 16 * ((h + 15) // 16)) > 512, "scene must give long tile lists"
+    errs = G.check_image(_outputs(out), ref) + G.check_projection(_outputs(out), ref)
+    ds, dr = G.oracle().covariance_backward(sc.scaling.numpy(), sc.rotation.numpy(), ref["grads"]["cov3d"])
+    errs += G.check_grad("xyz", _np(m._xyz.grad), ref["grads"]["xyz"])
+    errs += G.check_grad("scaling", _np(m._scaling.grad), ds)
+    errs += G.check_grad("rotation", _np(m._rotation.grad), dr)
+    errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"])
+    assert not errs, errs
