@@ -235,3 +235,37 @@ def test_long_tile_lists_vs_oracle(pkg, cuda, bg):
     errs += G.check_grad("rotation", _np(m._rotation.grad), dr)
     errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"])
     assert not errs, errs
+
+
+def test_c3_full_size_vs_oracle(pkg, cuda):
+    """BASELINE config C3 (1M Gaussians, 1920x1080): full frame, fwd + bwd, vs
+    the oracle (OpenMP).  Pixel-exact decisions are expected; the tolerance
+    admits a few knife-edge pixels (w ~ 1e-5 or A ~ 0.995 within rounding)."""
+    import os
+    syn = pkg.synthetic
+    W, H = 1920, 1080
+    sc = syn.make_scene(1_000_000, W, H, seed=0)
+    m = syn.to_model(sc, pkg.GaussianModel, cuda)
+    out = pkg.GaussianRenderer().render(Cam(W, H, sc.fovx, sc.fovy), m, pkg.RenderSettings(H, W, torch.zeros(3)))
+    rng = np.random.default_rng(1)
+    gi, ga, gd = (rng.uniform(-1, 1, s).astype(np.float32) for s in ((3, H, W), (1, H, W), (1, H, W)))
+    L = sum((out[k] * torch.tensor(v, device=cuda)).sum() for k, v in (("image", gi), ("alpha", ga), ("depth", gd)))
+    L.backward()
+    cov = G.oracle().covariance(sc.scaling.numpy(), sc.rotation.numpy())
+    ref = G.oracle().render_backward(_oracle_scene(sc, cov, (0.0, 0.0, 0.0)), gi, ga, gd,
+                                     nthreads=min(16, os.cpu_count() or 1))
+    o = _outputs(out)
+    assert np.array_equal(o["vis"], ref["vis"])
+    bad = (np.abs(o["image"] - ref["image"]) > 1e-4).any(0) | (np.abs(o["alpha"] - ref["alpha"]) > 1e-4)[0]
+    print(f"C3: {int(bad.sum())} of {H * W} pixels over 1e-4; max image err "
+          f"{G.max_err(o['image'], ref['image']):.3g}; T={ref['T']} E={ref['E']} C={ref['C']}")
+    assert bad.mean() < 1e-5, f"{int(bad.sum())} pixels over 1e-4"
+    ds, dr = G.oracle().covariance_backward(sc.scaling.numpy(), sc.rotation.numpy(), ref["grads"]["cov3d"])
+    for name, d, r in (("xyz", _np(m._xyz.grad), ref["grads"]["xyz"]), ("scaling", _np(m._scaling.grad), ds),
+                       ("rotation", _np(m._rotation.grad), dr)):
+        print(f"C3 grad {name}: max err / max|ref| = {G.max_err(d, r) / np.abs(r).max():.3g}")
+    errs = G.check_grad("xyz", _np(m._xyz.grad), ref["grads"]["xyz"])
+    errs += G.check_grad("scaling", _np(m._scaling.grad), ds)
+    errs += G.check_grad("rotation", _np(m._rotation.grad), dr)
+    errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"])
+    assert not errs, errs
