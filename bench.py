@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-optimizer", action="store_true", help="time render fwd+bwd only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI) for the driver; gloo only to rehearse N>1 on one GPU")
     return ap.parse_args()
 
 
@@ -93,12 +95,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))  # % only matters for a 1-GPU gloo rehearsal
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
 
     W, H, n = a.width, a.height, a.gaussians
     scene = pkg.synthetic.make_scene(n, W, H, seed=0)

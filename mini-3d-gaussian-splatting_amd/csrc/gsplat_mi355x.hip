@@ -726,7 +726,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         P = __builtin_fmaf(c, X, P);
         // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
         const bool term = A >= kAlphaStop;
-        const float inv = __frcp_rn(1.f - A);
+        const float inv = __builtin_amdgcn_rcpf(1.f - A);  // v_rcp_f32 (1 ulp): a gradient factor, no decision
         const float dal = trans * (term ? X + gA : __builtin_fmaf(inv, __builtin_fmaf(gA, onemA, P - K), X));
         const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
         dop = take ? du * w : 0.f;
