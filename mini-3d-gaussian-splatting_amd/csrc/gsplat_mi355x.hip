@@ -503,11 +503,14 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
   tile_pixel(tile, a.tiles_x, px, py);
   const int W = a.cam.image_width, H = a.cam.image_height;
   const bool inside = px < W && py < H;
-  const uint32_t start = a.ranges[2 * tile], end = a.ranges[2 * tile + 1];
+  const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]),
+                 end = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
   float ar = bg0, ag = bg1, ab = bg2;  // out_rgb = bg (renderer.py:273)
-  float A = 0.f, D = 0.f;
-  bool done = !inside;
+  // A lane is done once A >= kAlphaStop (A only grows through accepted
+  // pairs, so that is exactly the :352 break); lanes outside the image start
+  // done.  No loop-carried bool: "done" is one compare, not a mask in SGPRs.
+  float A = inside ? 0.f : 1.f, D = 0.f;
   uint32_t neval = 0;
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
@@ -521,7 +524,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
     n2 = recs[3 * (size_t)gid + 2];
   }
   for (uint32_t b = start; b < end; b += kBlock) {
-    const uint32_t cnt = min((uint32_t)kBlock, end - b);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(min((uint32_t)kBlock, end - b));
     {  // (the previous round ended in a barrier after its last LDS read)
       float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * threadIdx.x]);
       d[0] = n0;
@@ -537,13 +540,13 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
     }
     // Control flow stays wave-uniform (ballots); per-lane decisions are
     // predicates, and a skipped pair adds exact zeros.
-    if (wave_any(!done)) {
+    if (wave_any(A < kAlphaStop)) {
       for (uint32_t j = 0; j < cnt; ++j) {
         const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
         const float dx = fx - pm.x, dy = fy - pm.y;
         const float s = ((dx * dx) * pq.x + (pq.y * dx) * dy) + (dy * dy) * po.x;  // :333
         // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp
-        const bool live = !done && !(s > 23.1f);
+        const bool live = A < kAlphaStop && !(s > 23.1f);
         if (wave_any(live)) {
           const float w = sat01(exp_inrange(-0.5f * s));  // :334
           const float ai = sat01(po.y * w);                // :339
@@ -559,14 +562,13 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
           D += c * pbz.y;
           const bool term = take && A >= kAlphaStop;  // :352 (after accumulation)
           neval = term ? b - start + j + 1 : neval;
-          done = done || term;
-          if (!wave_any(!done)) break;
+          if (!wave_any(A < kAlphaStop)) break;
         }
       }
     }
     // all pixels of the tile done? (per-wave ballot -- taken with every lane
     // active, outside the lane-0 branch -- then the 4 wave flags)
-    const bool wave_live = wave_any(!done);
+    const bool wave_live = wave_any(A < kAlphaStop);
     if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = wave_live ? 1u : 0u;
     lds_barrier();
     const uint32_t any_live = s_live[0] | s_live[1] | s_live[2] | s_live[3];
@@ -574,7 +576,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
     if (!any_live) break;
   }
   if (!inside) return;
-  if (!done) neval = end - start;
+  if (A < kAlphaStop) neval = end - start;
   const size_t HW = (size_t)W * H, p = (size_t)py * W + px;
   const float tb = 1.f - A;
   a.image[p] = clamp01(ar + tb * bg0);  // :359,364
@@ -629,7 +631,8 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   tile_pixel(tile, a.tiles_x, px, py);
   const int W = a.cam.image_width, H = a.cam.image_height;
   const bool inside = px < W && py < H;
-  const uint32_t start = a.ranges[2 * tile], end = a.ranges[2 * tile + 1];
+  const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]),
+                 end = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
   if (tid == 0) s_max = 0;
   // pixel cotangents through clamp / bg composite / depth normalisation
@@ -661,7 +664,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   __syncthreads();
   if (neval) atomicMax(&s_max, neval);
   __syncthreads();
-  const uint32_t stop = start + s_max;
+  const uint32_t stop = start + __builtin_amdgcn_readfirstlane(s_max);  // uniform: scalar loop bounds
   const float onemA = 1.f - At;
   // Suffix sums without per-channel state: with X_i = gR . col_i + gD z_i,
   //   sum_k gR_k (accT_k - acc_k) + gD (Dt - D) = K - P,
@@ -683,7 +686,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   }
   const uint32_t tile_x = (uint32_t)(tile % a.tiles_x), tile_y = (uint32_t)(tile / a.tiles_x);
   for (uint32_t b = start; b < stop; b += kBwdBatch) {
-    const uint32_t cnt = min((uint32_t)kBwdBatch, stop - b);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(min((uint32_t)kBwdBatch, stop - b));
     lds_barrier();  // previous phase B done with s_rec, s_e, s_dop, s_c
     if (tid < kBwdBatch) {
       float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * tid]);
@@ -726,11 +729,15 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         P = __builtin_fmaf(c, X, P);
         // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
         const bool term = A >= kAlphaStop;
+        // both arms computed, then a select: no divergent branch per entry
         const float inv = __builtin_amdgcn_rcpf(1.f - A);  // v_rcp_f32 (1 ulp): a gradient factor, no decision
-        const float dal = trans * (term ? X + gA : __builtin_fmaf(inv, __builtin_fmaf(gA, onemA, P - K), X));
-        const float du = (u >= 0.f && u <= 1.f) ? dal : 0.f;
-        dop = take ? du * w : 0.f;
-        cw = take ? ((e >= 0.f && e <= 1.f) ? c : -c) : 0.f;
+        const float d_live = __builtin_fmaf(inv, __builtin_fmaf(gA, onemA, P - K), X);
+        const float d_term = X + gA;
+        const float dal = trans * (term ? d_term : d_live);
+        // u = o*w >= 0, so "u in [0,1]" (the clamp passes the gradient) is ai == u;
+        // e = exp(.) >= 0, so "e in [0,1]" is w == e (both false for NaN)
+        dop = (take && ai == u) ? dal * w : 0.f;
+        cw = (w == e) ? c : -c;  // c == 0 when !take
       }
       s_dop[j][tid] = dop;
       s_c[j][tid] = cw;
