@@ -486,6 +486,37 @@ __device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int &px, int &
   py = ty * GS_TILE + ((wave >> 1) << 3) + (lane >> 3);
 }
 
+// Wave-level culling of list entries.  Bit q of the result is clear only if
+// every pixel centre of the tile's 8x8 quadrant q = (q&1, q>>1) provably has
+// s > 23.1, i.e. exp(-s/2) < 1e-5 (the :336 skip): that wave may pass the
+// entry over without evaluating it (each lane's own exact test still decides
+// the rest).  The s <= L ellipse, L = 23.1 * 1.01, lies in the box
+// |x - mx| <= sqrt(L Sxx), |y - my| <= sqrt(L Syy), Sigma = Q^-1 for the form
+// Q = [[q00, qo/2], [qo/2, q11]] the blend evaluates.  The 1% margin covers
+// the fp32 rounding of s: |s_fp32 - s| <= ~4u (q00 dx^2 + |qo dx dy| + q11 dy^2)
+// <= 4u (tr + |qo|) tr / det * s, so conics with (tr + |qo|) tr > 1e4 det --
+// and non-positive-definite or NaN ones -- keep all four bits.
+__device__ __forceinline__ uint32_t quad_mask(float mx, float my, float q00, float qo, float q11, float x0,
+                                              float y0) {
+  const float q01 = 0.5f * qo;
+  const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
+  if (!(tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det)) return 0xFu;
+  const float L = 23.1f * 1.01f;
+  // v_rcp / v_sqrt (~1 ulp): far inside the 1% margin
+  const float id = __builtin_amdgcn_rcpf(det);
+  const float hx = __builtin_amdgcn_sqrtf(L * q11 * id), hy = __builtin_amdgcn_sqrtf(L * q00 * id);
+  const bool x0h = mx + hx >= x0 && mx - hx <= x0 + 7.f, x1h = mx + hx >= x0 + 8.f && mx - hx <= x0 + 15.f;
+  const bool y0h = my + hy >= y0 && my - hy <= y0 + 7.f, y1h = my + hy >= y0 + 8.f && my - hy <= y0 + 15.f;
+  return (uint32_t)(x0h && y0h) | ((uint32_t)(x1h && y0h) << 1) | ((uint32_t)(x0h && y1h) << 2) |
+         ((uint32_t)(x1h && y1h) << 3);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
+  return v;
+}
+
 // Records staged in LDS are read as 8-byte pairs: ds_read_b64 costs 2 LDS
 // cycles per wave-instruction (broadcast), ds_read_b96 8 and ds_read_b128 4
 // (MI355X_MICROARCH.md, LDS table): (mx,my) (q00,qo) (q11,o) | (r,g) (b,z).
@@ -515,6 +546,10 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   __shared__ uint32_t s_live[4];
+  // s_qm[q][w]: bit i set if entry 64w+i of the batch may reach quadrant q
+  __shared__ unsigned long long s_qm[4][4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float tx0 = (float)((tile % a.tiles_x) * GS_TILE), ty0 = (float)((tile / a.tiles_x) * GS_TILE);
   // batch i+1's records are gathered into registers while batch i composites
   float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
   if (start + threadIdx.x < end) {
@@ -524,12 +559,17 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
     n2 = recs[3 * (size_t)gid + 2];
   }
   for (uint32_t b = start; b < end; b += kBlock) {
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(min((uint32_t)kBlock, end - b));
     {  // (the previous round ended in a barrier after its last LDS read)
       float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * threadIdx.x]);
       d[0] = n0;
       d[1] = n1;
       d[2] = n2;
+      const uint32_t qm = (b + threadIdx.x < end) ? quad_mask(n0.x, n0.y, n0.z, n0.w, n1.x, tx0, ty0) : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned long long bq = __builtin_amdgcn_ballot_w64((qm >> q) & 1u);
+        if (lane == 0) s_qm[q][wave] = bq;
+      }
     }
     lds_barrier();
     if (b + kBlock + threadIdx.x < end) {
@@ -538,10 +578,22 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
       n1 = recs[3 * (size_t)gid + 1];
       n2 = recs[3 * (size_t)gid + 2];
     }
-    // Control flow stays wave-uniform (ballots); per-lane decisions are
-    // predicates, and a skipped pair adds exact zeros.
-    if (wave_any(A < kAlphaStop)) {
-      for (uint32_t j = 0; j < cnt; ++j) {
+    // Control flow stays wave-uniform (ballots, scalar bit scans over the
+    // quadrant masks); per-lane decisions are predicates, and a skipped pair
+    // adds exact zeros.
+    // The "every lane done" exit is tested once per 64-entry word: past it
+    // an entry costs only the s test (A >= kAlphaStop fails every lane), far
+    // less than a per-entry ballot + branch on the whole list.
+    for (int wd = 0; wd < 4; ++wd) {
+      if (!wave_any(A < kAlphaStop)) break;
+      const unsigned long long mw = s_qm[wave][wd];
+      // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+      unsigned long long m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mw >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mw);
+      while (m) {
+        const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+        m &= ~(1ull << bit);
+        const uint32_t j = 64u * wd + bit;
         const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
         const float dx = fx - pm.x, dy = fy - pm.y;
         const float s = ((dx * dx) * pq.x + (pq.y * dx) * dy) + (dy * dy) * po.x;  // :333
@@ -549,20 +601,21 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         const bool live = A < kAlphaStop && !(s > 23.1f);
         if (wave_any(live)) {
           const float w = sat01(exp_inrange(-0.5f * s));  // :334
-          const float ai = sat01(po.y * w);                // :339
-          const float c0 = (1.f - A) * ai;                   // :343-344
-          // :336 / :340 / :345 skips
-          const bool take = live && !(w < kMinWeight) && !(ai <= 0.f) && !(c0 <= 0.f);
-          const float c = take ? c0 : 0.f;
+          // :336 / :340 / :345 skips folded into the weight: a skipped pair
+          // gets ai = 0, hence c = (1 - A) * 0 = +0 (1 - A >= 0), and an
+          // accepted one c = (1 - A) * ai > 0 -- the reference's c exactly.
+          // Selects (v_cndmask) instead of SGPR mask arithmetic.
+          const float ai = (live && !(w < kMinWeight)) ? sat01(po.y * w) : 0.f;  // :339
+          const float c = (1.f - A) * ai;                                        // :343-344
           const float2 prg = lds_pair(&s_rec[6 * j + 3]), pbz = lds_pair(&s_rec[6 * j + 4]);
+          const float A0 = A;
           ar += c * prg.x;
           ag += c * prg.y;
           ab += c * pbz.x;
           A = A + c;
           D += c * pbz.y;
-          const bool term = take && A >= kAlphaStop;  // :352 (after accumulation)
-          neval = term ? b - start + j + 1 : neval;
-          if (!wave_any(A < kAlphaStop)) break;
+          // :352 (after accumulation): the lane's terminating entry
+          neval = (A0 < kAlphaStop && A >= kAlphaStop) ? b - start + j + 1 : neval;
         }
       }
     }
@@ -619,14 +672,18 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// Occupancy: the LDS footprint (~39 KB) allows 4 blocks per CU, i.e. 4 waves
+// per SIMD, which needs <= 128 VGPRs (phase B's unroll sets the peak).
 __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float2 s_rec[kBwdBatch * 6];
   __shared__ uint32_t s_e[kBwdBatch];
   __shared__ float s_dop[kBwdBatch][kPdStride], s_c[kBwdBatch][kPdStride];
   __shared__ float4 s_pg[kBlock];   // per pixel: dL/drgb (masked), dL/dD
   __shared__ uint32_t s_max;
+  __shared__ uint32_t s_qmb[4];     // bit j: batch entry j may reach quadrant q (quad_mask)
   const int tile = blockIdx.x;
   const int tid = threadIdx.x;
+  const int wave = tid >> 6;
   int px, py;
   tile_pixel(tile, a.tiles_x, px, py);
   const int W = a.cam.image_width, H = a.cam.image_height;
@@ -662,7 +719,9 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   const float fx = (float)px, fy = (float)py;
   s_pg[tid] = make_float4(gR0, gR1, gR2, gD);
   __syncthreads();
-  if (neval) atomicMax(&s_max, neval);
+  // this wave's last evaluated entry, and the tile's
+  const uint32_t wstop = __builtin_amdgcn_readfirstlane(wave_max_u32(neval));
+  if ((tid & 63) == 0 && wstop) atomicMax(&s_max, wstop);
   __syncthreads();
   const uint32_t stop = start + __builtin_amdgcn_readfirstlane(s_max);  // uniform: scalar loop bounds
   const float onemA = 1.f - At;
@@ -697,18 +756,37 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       const uint32_t info = __float_as_uint(n2.w);
       s_e[tid] = __float_as_uint(n2.z) + (tile_y - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
                  (tile_x - (info & 0xFFFu));
-      if (b + kBwdBatch + tid < stop) {
-        const uint32_t gid = a.sorted_gauss[b + kBwdBatch + tid];
-        n0 = recs[3 * (size_t)gid];
-        n1 = recs[3 * (size_t)gid + 1];
-        n2 = recs[3 * (size_t)gid + 2];
+    }
+    if (tid < 64) {  // wave 0: the batch's quadrant masks
+      const uint32_t qm = (tid < kBwdBatch && b + tid < stop)
+                              ? quad_mask(n0.x, n0.y, n0.z, n0.w, n1.x, (float)(tile_x * GS_TILE), (float)(tile_y * GS_TILE))
+                              : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t bq = (uint32_t)__builtin_amdgcn_ballot_w64((qm >> q) & 1u);
+        if (tid == 0) s_qmb[q] = bq;
       }
+    }
+    if (tid < kBwdBatch && b + kBwdBatch + tid < stop) {
+      const uint32_t gid = a.sorted_gauss[b + kBwdBatch + tid];
+      n0 = recs[3 * (size_t)gid];
+      n1 = recs[3 * (size_t)gid + 1];
+      n2 = recs[3 * (size_t)gid + 2];
     }
     lds_barrier();
     // ---- phase A: replay ------------------------------------------------
     const uint32_t jbase = b - start;
+    // entries this wave evaluates: inside its own last evaluated entry and
+    // not culled for its quadrant; the others only store zeros
+    const uint32_t lim = wstop > jbase ? min(wstop - jbase, 32u) : 0u;
+    const uint32_t qw = __builtin_amdgcn_readfirstlane(s_qmb[wave]) & (lim >= 32u ? ~0u : ((1u << lim) - 1u));
     for (uint32_t j = 0; j < cnt; ++j) {
       float dop = 0.f, cw = 0.f;
+      if (!((qw >> j) & 1u)) {
+        s_dop[j][tid] = 0.f;
+        s_c[j][tid] = 0.f;
+        continue;
+      }
       const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
       const float dx = fx - pm.x, dy = fy - pm.y;
       const float sq = ((dx * dx) * pq.x + (pq.y * dx) * dy) + (dy * dy) * po.x;
@@ -772,6 +850,9 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         g7 = __builtin_fmaf(pg.y, cw, g7);
         g8 = __builtin_fmaf(pg.z, cw, g8);
         g9 = __builtin_fmaf(pg.w, cw, g9);
+        // keep the second half's LDS reads below this point: hoisting all 48
+        // of them needs > 128 VGPRs (fewer than 4 waves per SIMD)
+        if (kk == 7) __builtin_amdgcn_sched_barrier(0);
       }
       Sx = row16_sum(Sx); Sy = row16_sum(Sy); g2 = row16_sum(g2); g3 = row16_sum(g3); g4 = row16_sum(g4);
       g5 = row16_sum(g5); g6 = row16_sum(g6); g7 = row16_sum(g7); g8 = row16_sum(g8); g9 = row16_sum(g9);

@@ -3,6 +3,8 @@ reference's golden vectors and the pinned CPU oracle.
 
 Tolerances are in tests/golden_io.py (1e-4 abs on image/alpha, gated depth,
 grads 2e-3 x max|ref| + 1e-5)."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -147,6 +149,46 @@ def test_random_scene_vs_oracle(pkg, cuda, n, w, h, sig):
     errs += G.check_grad("rotation", _np(m._rotation.grad), dr)
     errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"])
     errs += G.check_grad("opacity", _np(m._opacity.grad)[:, 0], ref["grads"]["opacity"] * op * (1 - op))
+    assert not errs, errs
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_needle_gaussians_vs_oracle(pkg, cuda, seed):
+    """Needle-shaped Gaussians (one axis 25-2000x the others): 2D conics with
+    condition numbers on both sides of the blend's wave-culling limit
+    (quad_mask), whose exp(-s/2) >= 1e-5 region reaches well past the 3-sigma
+    rectangle they are binned by.  Both sides project the SAME fp32 cov3d
+    (the reference's get_covariance path): building a covariance this
+    ill-conditioned amplifies a 1-ulp exp() difference beyond any tolerance."""
+    syn = pkg.synthetic
+    n, w, h = 4000, 160, 128
+    sc = syn.make_scene(n, w, h, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    sc.scaling[:, 0] = torch.empty(n).uniform_(math.log(0.05), math.log(0.2), generator=g)
+    sc.scaling[:, 1:] = torch.empty(n, 2).uniform_(math.log(1e-4), math.log(2e-3), generator=g)
+    cov = G.oracle().covariance(sc.scaling.numpy(), sc.rotation.numpy())
+    op = torch.sigmoid(sc.opacity[:, 0]).numpy()
+    bg = [0.2, 0.1, 0.0]
+    gs = Gauss(sc.xyz.numpy(), cov, sc.features_dc[:, 0].numpy(), op, cuda)
+    out = pkg.GaussianRenderer().render(Cam(w, h, sc.fovx, sc.fovy), gs, pkg.RenderSettings(h, w, torch.tensor(bg)))
+    rng = np.random.default_rng(seed)
+    gi, ga, gd = (rng.uniform(-1, 1, s).astype(np.float32) for s in ((3, h, w), (1, h, w), (1, h, w)))
+    L = sum((out[k] * torch.tensor(v, device=cuda)).sum() for k, v in (("image", gi), ("alpha", ga), ("depth", gd)))
+    L.backward()
+    ref = G.oracle().render_backward(_oracle_scene(sc, cov, bg), gi, ga, gd)
+    errs = G.check_image(_outputs(out), ref) + G.check_projection(_outputs(out), ref)
+    errs += G.check_grad("xyz", _np(gs.xyz.grad), ref["grads"]["xyz"])
+    errs += G.check_grad("features_dc", _np(gs.feats.grad)[:, 0], ref["grads"]["color_logits"])
+    errs += G.check_grad("opacity", _np(gs.op.grad)[:, 0], ref["grads"]["opacity"])
+    # dL/dcov3d = J^T (-Q G Q) J R-rotated: an fp32 summation-order difference
+    # in G = dL/dconic (tile pairs summed in another order) is amplified by
+    # cond(Q)^2, so it is compared where the 2D conic is well conditioned
+    q = ref["conics"].reshape(n, 4).astype(np.float64)
+    hm, hd = 0.5 * (q[:, 0] + q[:, 3]), np.sqrt((0.5 * (q[:, 0] - q[:, 3])) ** 2 + q[:, 1] * q[:, 2])
+    cond = (hm + hd) / np.maximum(hm - hd, 1e-30)
+    well = cond < 1e3
+    assert well.sum() > 100 and (~well & ref["vis"].astype(bool)).sum() > 50, "both conditioning regimes covered"
+    errs += G.check_grad("cov3d", _np(gs.cov.grad).reshape(n, 9)[well], ref["grads"]["cov3d"].reshape(n, 9)[well])
     assert not errs, errs
 
 

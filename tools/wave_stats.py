@@ -54,7 +54,8 @@ def main():
     qmax = pad.view(ty_n, 2, 8, tx_n, 2, 8).amax(dim=(2, 5))  # [ty, qy, tx, qx]
     qmax = qmax.permute(0, 2, 1, 3).reshape(ty_n * tx_n, 4)    # quadrant q = qx + 2 qy
     L = 23.1 * 1.001
-    tot = {k: torch.zeros((), dtype=torch.long, device=dev) for k in ("processed", "live", "bbox", "live_notbbox")}
+    tot = {k: torch.zeros((), dtype=torch.long, device=dev)
+           for k in ("processed", "live", "bbox", "live_notbbox", "bwd_lockstep", "bwd_max", "bwd_sum")}
     ys, xs = torch.meshgrid(torch.arange(8, device=dev), torch.arange(8, device=dev), indexing="ij")
     ys, xs = ys.reshape(-1).float(), xs.reshape(-1).float()
     num_tiles = tx_n * ty_n
@@ -88,8 +89,23 @@ def main():
             tot["live"] += live.sum()
             tot["bbox"] += (proc & bb).sum()
             tot["live_notbbox"] += (live & ~bb).sum()
+            # backward: batches of 16 up to the tile's deepest entry; per batch
+            # a lockstep block pays 16 entries in every wave (no culling), the
+            # culled block the busiest wave's count, decoupled waves their own
+            stop = int(qmax[t].max())
+            if stop > 0:
+                work = (proc & bb)[:stop].float()                     # [stop, 4]
+                nb = (stop + 15) // 16
+                wpad = torch.zeros(nb * 16, 4, device=dev)
+                wpad[:stop] = work
+                per = wpad.view(nb, 16, 4).sum(1)                     # [nb, 4]
+                tot["bwd_lockstep"] += 4 * stop
+                tot["bwd_max"] += (4 * per.max(1).values).sum().long()
+                tot["bwd_sum"] += per.sum().long()
     tot = {k: int(v) for k, v in tot.items()}
     print(tot)
+    print(f"backward phase-A wave-entries: lockstep {tot['bwd_lockstep']}, culled+barrier {tot['bwd_max']}, "
+          f"decoupled {tot['bwd_sum']}")
     p = tot["processed"]
     print(f"live/processed = {tot['live'] / p:.3f}, bbox/processed = {tot['bbox'] / p:.3f}, "
           f"evaluated pairs (E) = {int(neval.sum())}, processed lane-pairs = {64 * p}")
