@@ -798,9 +798,9 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         const float u = po.y * w;
         const float ai = sat01(u);
         const float trans = 1.f - A;
-        const float c0 = trans * ai;
-        const bool take = live && !(w < kMinWeight) && !(ai <= 0.f) && !(c0 <= 0.f);  // the forward's skips
-        const float c = take ? c0 : 0.f;
+        // the forward's skips folded into the weight exactly as there: c is
+        // +0 for a skipped pair and > 0 for an accepted one (take <=> c > 0)
+        const float c = trans * ((live && !(w < kMinWeight)) ? ai : 0.f);
         const float2 prg = lds_pair(&s_rec[6 * j + 3]), pbz = lds_pair(&s_rec[6 * j + 4]);
         const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
         A = A + c;
@@ -814,8 +814,9 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         const float dal = trans * (term ? d_term : d_live);
         // u = o*w >= 0, so "u in [0,1]" (the clamp passes the gradient) is ai == u;
         // e = exp(.) >= 0, so "e in [0,1]" is w == e (both false for NaN)
-        dop = (take && ai == u) ? dal * w : 0.f;
-        cw = (w == e) ? c : -c;  // c == 0 when !take
+        const float g = (ai == u) ? dal * w : 0.f;
+        dop = (c > 0.f) ? g : 0.f;
+        cw = (w == e) ? c : -c;  // c == +0 when skipped
       }
       s_dop[j][tid] = dop;
       s_c[j][tid] = cw;
