@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 #define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_MAX_RECT_TILES 8   /* r <= 50 px -> an AABB spans at most 8 tiles per axis */
@@ -170,8 +170,18 @@ typedef struct gs_blend_fwd_args {
   float *depth;                 /* [H,W]   */
   float *pix_acc;               /* [H*W,4] */
   float *pix_state;             /* [H*W,2] */
+  uint64_t *live_bits;          /* [4, live_words]: see gs_blend_live_words */
+  int64_t live_words;
 } gs_blend_fwd_args;
 gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
+
+/* Words per quadrant of the liveness bitmap the forward writes for the
+ * backward: bit i of live_bits[q * live_words + ranges[2t] / 64 + t + i / 64]
+ * is set iff list entry i of tile t reached (exp(-s/2) >= 1e-5) some
+ * still-running pixel of the tile's 8x8 quadrant q = (qx + 2 qy) -- the
+ * backward replays exactly those (entry, quadrant) pairs.  Bits past a
+ * quadrant's last evaluated entry are left unwritten. */
+size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles);
 
 /* ---- Backward of the blend -------------------------------------------
  * Re-walks each pixel's list front-to-back (bit-identical replay of the
@@ -190,6 +200,8 @@ typedef struct gs_blend_bwd_args {
   const float *g_image;         /* [3,H,W] dL/dimage */
   const float *g_alpha;         /* [H,W] or NULL */
   const float *g_depth;         /* [H,W] or NULL */
+  const uint64_t *live_bits;    /* the forward's liveness bitmap */
+  int64_t live_words;
   float *pair_grads;            /* [T, GS_PAIR_GRAD_FLOATS] */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);

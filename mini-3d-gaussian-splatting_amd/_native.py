@@ -24,7 +24,7 @@ GS_TILE = 16
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 1
+GS_ABI_VERSION = 2
 
 _vp = C.c_void_p
 
@@ -71,7 +71,7 @@ class GsBlendFwdArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
         ("sorted_gauss", _vp), ("records", _vp), ("image", _vp), ("alpha", _vp), ("depth", _vp),
-        ("pix_acc", _vp), ("pix_state", _vp),
+        ("pix_acc", _vp), ("pix_state", _vp), ("live_bits", _vp), ("live_words", C.c_int64),
     ]
 
 
@@ -80,7 +80,7 @@ class GsBlendBwdArgs(C.Structure):
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
         ("sorted_gauss", _vp), ("records", _vp), ("pix_acc", _vp),
         ("pix_state", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp),
-        ("pair_grads", _vp),
+        ("live_bits", _vp), ("live_words", C.c_int64), ("pair_grads", _vp),
     ]
 
 
@@ -114,7 +114,8 @@ class GsAdamArgs(C.Structure):
 EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
-    "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward", "gs_adam_step",
+    "gs_tile_ranges", "gs_blend_live_words", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
+    "gs_adam_step",
 )
 
 _lib = None
@@ -139,6 +140,8 @@ def _declare(lib):
     lib.gs_bin_count.argtypes = [P(GsBinArgs), _vp]
     lib.gs_bin_emit.argtypes = [P(GsBinArgs), _vp]
     lib.gs_tile_ranges.argtypes = [P(GsRangeArgs), _vp]
+    lib.gs_blend_live_words.argtypes = [C.c_int32, C.c_int32]
+    lib.gs_blend_live_words.restype = C.c_size_t
     lib.gs_blend_forward.argtypes = [P(GsBlendFwdArgs), _vp]
     lib.gs_blend_backward.argtypes = [P(GsBlendBwdArgs), _vp]
     lib.gs_project_backward.argtypes = [P(GsProjectBwdArgs), _vp]

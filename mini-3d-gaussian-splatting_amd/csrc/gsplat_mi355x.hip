@@ -584,8 +584,11 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
     // The "every lane done" exit is tested once per 64-entry word: past it
     // an entry costs only the s test (A >= kAlphaStop fails every lane), far
     // less than a per-entry ballot + branch on the whole list.
+    // liveness word of (this batch, word wd, this quadrant): see gs_blend_live_words
+    const uint64_t live_word0 = (uint64_t)start / 64u + (uint64_t)tile + (uint64_t)(b - start) / 64u;
     for (int wd = 0; wd < 4; ++wd) {
       if (!wave_any(A < kAlphaStop)) break;
+      unsigned long long livem = 0;  // entries some lane of this wave evaluated
       const unsigned long long mw = s_qm[wave][wd];
       // (readfirstlane returns int: widen through uint32_t, never sign-extend)
       unsigned long long m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mw >> 32)) << 32) |
@@ -600,6 +603,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp
         const bool live = A < kAlphaStop && !(s > 23.1f);
         if (wave_any(live)) {
+          livem |= 1ull << bit;
           const float w = sat01(exp_inrange(-0.5f * s));  // :334
           // :336 / :340 / :345 skips folded into the weight: a skipped pair
           // gets ai = 0, hence c = (1 - A) * 0 = +0 (1 - A >= 0), and an
@@ -618,6 +622,9 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
           neval = (A0 < kAlphaStop && A >= kAlphaStop) ? b - start + j + 1 : neval;
         }
       }
+      // (only words inside the tile's list: the next tile's words follow)
+      if (lane == 0 && b - start + 64u * wd < end - start && live_word0 + wd < (uint64_t)a.live_words)
+        a.live_bits[(size_t)wave * a.live_words + live_word0 + wd] = livem;
     }
     // all pixels of the tile done? (per-wave ballot -- taken with every lane
     // active, outside the lane-0 branch -- then the 4 wave flags)
@@ -680,7 +687,6 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float s_dop[kBwdBatch][kPdStride], s_c[kBwdBatch][kPdStride];
   __shared__ float4 s_pg[kBlock];   // per pixel: dL/drgb (masked), dL/dD
   __shared__ uint32_t s_max;
-  __shared__ uint32_t s_qmb[4];     // bit j: batch entry j may reach quadrant q (quad_mask)
   const int tile = blockIdx.x;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -757,16 +763,6 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       s_e[tid] = __float_as_uint(n2.z) + (tile_y - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
                  (tile_x - (info & 0xFFFu));
     }
-    if (tid < 64) {  // wave 0: the batch's quadrant masks
-      const uint32_t qm = (tid < kBwdBatch && b + tid < stop)
-                              ? quad_mask(n0.x, n0.y, n0.z, n0.w, n1.x, (float)(tile_x * GS_TILE), (float)(tile_y * GS_TILE))
-                              : 0u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t bq = (uint32_t)__builtin_amdgcn_ballot_w64((qm >> q) & 1u);
-        if (tid == 0) s_qmb[q] = bq;
-      }
-    }
     if (tid < kBwdBatch && b + kBwdBatch + tid < stop) {
       const uint32_t gid = a.sorted_gauss[b + kBwdBatch + tid];
       n0 = recs[3 * (size_t)gid];
@@ -778,8 +774,15 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
     const uint32_t jbase = b - start;
     // entries this wave evaluates: inside its own last evaluated entry and
     // not culled for its quadrant; the others only store zeros
+    // the forward's liveness bits of this wave's quadrant (64 % kBwdBatch == 0:
+    // a batch never straddles two words); bits past wstop were never written
     const uint32_t lim = wstop > jbase ? min(wstop - jbase, 32u) : 0u;
-    const uint32_t qw = __builtin_amdgcn_readfirstlane(s_qmb[wave]) & (lim >= 32u ? ~0u : ((1u << lim) - 1u));
+    uint32_t qw = 0;
+    if (lim) {
+      const unsigned long long lw = a.live_bits[(size_t)wave * a.live_words + start / 64u + (uint32_t)tile + jbase / 64u];
+      const uint32_t bits = (uint32_t)(lw >> (jbase & 63u)) & ((1u << kBwdBatch) - 1u);
+      qw = __builtin_amdgcn_readfirstlane(bits) & (lim >= 32u ? ~0u : ((1u << lim) - 1u));
+    }
     for (uint32_t j = 0; j < cnt; ++j) {
       float dop = 0.f, cw = 0.f;
       if (!((qw >> j) & 1u)) {
@@ -1234,12 +1237,18 @@ gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream) {
   return check_launch("gs_tile_ranges");
 }
 
+size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles) {
+  if (num_pairs < 0 || num_tiles < 0) return 0;
+  return (size_t)num_pairs / 64u + (size_t)num_tiles + 2u;
+}
+
 gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_forward");
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16", "gs_blend_forward");
   if (a->tiles_x != (int)div_up(a->cam.image_width, GS_TILE) || a->tiles_y != (int)div_up(a->cam.image_height, GS_TILE))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_forward");
-  if (!a->ranges || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_acc || !a->pix_state)
+  if (!a->ranges || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_acc || !a->pix_state ||
+      !a->live_bits || a->live_words <= 0)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_forward");
   hipStream_t s = (hipStream_t)stream;
   k_blend_fwd<<<a->tiles_x * a->tiles_y, kBlock, 0, s>>>(*a);
@@ -1251,7 +1260,8 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16", "gs_blend_backward");
   if (a->tiles_x != (int)div_up(a->cam.image_width, GS_TILE) || a->tiles_y != (int)div_up(a->cam.image_height, GS_TILE))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_backward");
-  if (!a->ranges || !a->records || !a->pix_acc || !a->pix_state || !a->g_image || !a->pair_grads)
+  if (!a->ranges || !a->records || !a->pix_acc || !a->pix_state || !a->g_image || !a->pair_grads ||
+      !a->live_bits || a->live_words <= 0)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_backward");
   hipStream_t s = (hipStream_t)stream;
   k_blend_bwd<<<a->tiles_x * a->tiles_y, kBlock, 0, s>>>(*a);

@@ -123,7 +123,7 @@ def _check_inputs(xyz: torch.Tensor):
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
     __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_acc",
-                 "pix_state", "M", "T")
+                 "pix_state", "live_bits", "M", "T")
 
 
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity):
@@ -206,14 +206,17 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     depth = torch.empty((1, H, W), dtype=f32, device=dev)
     pix_acc = torch.empty((H * W, 4), dtype=f32, device=dev)
     pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
+    live_words = int(lib.gs_blend_live_words(T, num_tiles))
+    live_bits = torch.empty((4, live_words), dtype=torch.int64, device=dev)
     fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), N.ptr(sorted_gauss), N.ptr(records),
-                          N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state))
+                          N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state),
+                          N.ptr(live_bits), live_words)
     StageTimer.mark("blend_fwd")
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
     StageTimer.mark("~end_fwd")
 
     fr.pair_offset, fr.ranges, fr.sorted_gauss = pair_offset, ranges, sorted_gauss
-    fr.pix_acc, fr.pix_state = pix_acc, pix_state
+    fr.pix_acc, fr.pix_state, fr.live_bits = pix_acc, pix_state, live_bits
     return image, alpha, depth, means2d, conics, radii, vis, fr
 
 
@@ -236,7 +239,8 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         pair_grads = torch.empty((max(fr.T, 1), N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
-                              N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(pair_grads))
+                              N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
+                              fr.live_bits.shape[1], N.ptr(pair_grads))
         StageTimer.mark("blend_bwd")
         N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
     raw = cov3d is None
