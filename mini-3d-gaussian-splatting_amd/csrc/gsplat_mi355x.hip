@@ -682,8 +682,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 // Occupancy: the LDS footprint (~39 KB) allows 4 blocks per CU, i.e. 4 waves
 // per SIMD, which needs <= 128 VGPRs (phase B's unroll sets the peak).
 __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
-  __shared__ float2 s_rec[kBwdBatch * 6];
-  __shared__ uint32_t s_e[kBwdBatch];
+  __shared__ float2 s_rec[2][kBwdBatch * 6];  // double-buffered: batch i+1 is staged during phase B(i)
+  __shared__ uint32_t s_e[2][kBwdBatch];
   __shared__ float s_dop[kBwdBatch][kPdStride], s_c[kBwdBatch][kPdStride];
   __shared__ float4 s_pg[kBlock];   // per pixel: dL/drgb (masked), dL/dD
   __shared__ uint32_t s_max;
@@ -750,32 +750,42 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
     n2 = recs[3 * (size_t)gid + 2];
   }
   const uint32_t tile_x = (uint32_t)(tile % a.tiles_x), tile_y = (uint32_t)(tile / a.tiles_x);
-  for (uint32_t b = start; b < stop; b += kBwdBatch) {
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(min((uint32_t)kBwdBatch, stop - b));
-    lds_barrier();  // previous phase B done with s_rec, s_e, s_dop, s_c
+  // Staging of a batch (threads < kBwdBatch): records into LDS and each
+  // entry's emit index, pair_offset[g] + the tile's index in g's rectangle.
+  auto stage = [&](int buf) {
     if (tid < kBwdBatch) {
-      float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * tid]);
+      float4 *d = reinterpret_cast<float4 *>(&s_rec[buf][6 * tid]);
       d[0] = n0;
       d[1] = n1;
       d[2] = n2;
-      // emit index of this entry: pair_offset[g] + the tile's index in g's rectangle
       const uint32_t info = __float_as_uint(n2.w);
-      s_e[tid] = __float_as_uint(n2.z) + (tile_y - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
-                 (tile_x - (info & 0xFFFu));
+      s_e[buf][tid] = __float_as_uint(n2.z) + (tile_y - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
+                      (tile_x - (info & 0xFFFu));
     }
-    if (tid < kBwdBatch && b + kBwdBatch + tid < stop) {
-      const uint32_t gid = a.sorted_gauss[b + kBwdBatch + tid];
+  };
+  auto prefetch = [&](uint32_t bn) {
+    if (tid < kBwdBatch && bn + tid < stop) {
+      const uint32_t gid = a.sorted_gauss[bn + tid];
       n0 = recs[3 * (size_t)gid];
       n1 = recs[3 * (size_t)gid + 1];
       n2 = recs[3 * (size_t)gid + 2];
     }
-    lds_barrier();
+  };
+  stage(0);
+  prefetch(start + kBwdBatch);
+  lds_barrier();
+  // Two barriers per batch: A(i) | X | stage(i+1) + B(i) | Y | A(i+1) ...
+  // Y orders B(i)'s reads of s_dop/s_c before A(i+1)'s writes and makes the
+  // staged batch visible; s_rec[buf^1] was last read by B(i-1), before X.
+  int buf = 0;
+  for (uint32_t b = start; b < stop; b += kBwdBatch, buf ^= 1) {
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(min((uint32_t)kBwdBatch, stop - b));
     // ---- phase A: replay ------------------------------------------------
     const uint32_t jbase = b - start;
-    // entries this wave evaluates: inside its own last evaluated entry and
-    // not culled for its quadrant; the others only store zeros
-    // the forward's liveness bits of this wave's quadrant (64 % kBwdBatch == 0:
-    // a batch never straddles two words); bits past wstop were never written
+    // entries this wave replays: the forward's liveness bits of its quadrant
+    // (64 % kBwdBatch == 0: a batch never straddles two words), cut at the
+    // wave's last evaluated entry (bits past it were never written); the
+    // other entries only store zeros
     const uint32_t lim = wstop > jbase ? min(wstop - jbase, 32u) : 0u;
     uint32_t qw = 0;
     if (lim) {
@@ -790,7 +800,8 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         s_c[j][tid] = 0.f;
         continue;
       }
-      const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
+      const float2 pm = lds_pair(&s_rec[buf][6 * j]), pq = lds_pair(&s_rec[buf][6 * j + 1]),
+                   po = lds_pair(&s_rec[buf][6 * j + 2]);
       const float dx = fx - pm.x, dy = fy - pm.y;
       const float sq = ((dx * dx) * pq.x + (pq.y * dx) * dy) + (dy * dy) * po.x;
       // exp(-11.55) < 1e-5: exact early skip (NaN falls through), as in the forward
@@ -804,7 +815,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         // the forward's skips folded into the weight exactly as there: c is
         // +0 for a skipped pair and > 0 for an accepted one (take <=> c > 0)
         const float c = trans * ((live && !(w < kMinWeight)) ? ai : 0.f);
-        const float2 prg = lds_pair(&s_rec[6 * j + 3]), pbz = lds_pair(&s_rec[6 * j + 4]);
+        const float2 prg = lds_pair(&s_rec[buf][6 * j + 3]), pbz = lds_pair(&s_rec[buf][6 * j + 4]);
         const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
         A = A + c;
         P = __builtin_fmaf(c, X, P);
@@ -824,10 +835,12 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       s_dop[j][tid] = dop;
       s_c[j][tid] = cw;
     }
-    lds_barrier();
+    lds_barrier();  // X
+    stage(buf ^ 1);
+    prefetch(b + 2 * kBwdBatch);
     // ---- phase B: per-entry sums ----------------------------------------
     if ((uint32_t)jj < cnt) {
-      const float2 pm = s_rec[6 * jj], pq = s_rec[6 * jj + 1], po = s_rec[6 * jj + 2];
+      const float2 pm = s_rec[buf][6 * jj], pq = s_rec[buf][6 * jj + 1], po = s_rec[buf][6 * jj + 2];
       const float mx = pm.x, my = pm.y, hop = -0.5f * po.y;
       // pixel p = sub + 16k sits at (tile_x0 + 8((k>>2)&1) + (sub&7), tile_y0 + 8(k>>3) + 2(k&3) + (sub>>3))
       const float bx = (float)((tile % a.tiles_x) * GS_TILE + (sub & 7)) - mx;
@@ -868,7 +881,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       if (sub == 0 && part == 0) {
         const float q00 = pq.x, qo = pq.y, q11 = po.x;
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
-        float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)s_e[jj] * GS_PAIR_GRAD_FLOATS);
+        float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)s_e[buf][jj] * GS_PAIR_GRAD_FLOATS);
         out[0] = make_float2(g0, g1);
         out[1] = make_float2(g2, g3);
         out[2] = make_float2(g4, g5);
@@ -876,6 +889,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         out[4] = make_float2(g8, g9);
       }
     }
+    lds_barrier();  // Y
   }
   // entries past every pixel's last evaluated pair carry no gradient
   const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
