@@ -918,11 +918,29 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
     unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
     const uint32_t cnt = rect_touches(tx0, tx1, ty0, ty1);
     const uint32_t off = a.pair_offset[g];
-    for (uint32_t e = off; e < off + cnt; ++e) {
-      const float2 *sl = reinterpret_cast<const float2 *>(a.pair_grads + (size_t)e * GS_PAIR_GRAD_FLOATS);
+    const float2 *sl = reinterpret_cast<const float2 *>(a.pair_grads + (size_t)off * GS_PAIR_GRAD_FLOATS);
+    constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
+    uint32_t e = 0;
+    // four slots' loads in flight per round trip (the summation order stays
+    // slot by slot)
+    for (; e + 4 <= cnt; e += 4) {
+      float2 v[4][kF2];
 #pragma unroll
-      for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) {
-        const float2 v = sl[k];
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < kF2; ++k) v[i][k] = sl[(e + i) * kF2 + k];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < kF2; ++k) {
+          acc[2 * k] += v[i][k].x;
+          acc[2 * k + 1] += v[i][k].y;
+        }
+    }
+    for (; e < cnt; ++e) {
+#pragma unroll
+      for (int k = 0; k < kF2; ++k) {
+        const float2 v = sl[e * kF2 + k];
         acc[2 * k] += v.x;
         acc[2 * k + 1] += v.y;
       }
