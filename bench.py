@@ -185,14 +185,18 @@ def main():
         # algorithmic bytes per launch
         bytes_fwd = 44 * R + 8 * num_tiles + 20 * H * W + 24 * H * W
         bytes_bwd = 44 * R + 4 * R + 40 * R + 8 * num_tiles + (24 + 20) * H * W
-        flops_fwd = 26 * E
-        kern = {"blend_fwd": (bytes_fwd, flops_fwd), "blend_bwd": (bytes_bwd, None)}
+        # algorithmic fp32 flops per evaluated pair:
+        # forward 26 (s, exp, alpha, composite); backward 66 (replay 26,
+        # alpha / colour / depth gradient 20, the 10 per-pair sums 20)
+        flops_fwd, flops_bwd = 26 * E, 66 * E
+        kern = {"blend_fwd": (bytes_fwd, flops_fwd), "blend_bwd": (bytes_bwd, flops_bwd)}
         dom = max((k for k in kern if k in stages), key=lambda k: stages[k])
         t_ms = stages[dom]
         ach = kern[dom][0] / (t_ms * 1e-3) / 1e9
+        traffic, tnote = pmc_traffic(dom)
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_ms": round(t_ms, 4),
-                "algorithmic_bytes_per_launch": int(kern[dom][0])}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tnote,
+                "avg_launch_ms": round(t_ms, 4), "algorithmic_bytes_per_launch": int(kern[dom][0])}
         if kern[dom][1]:
             tf = kern[dom][1] / (t_ms * 1e-3) / 1e12
             roof["valu"] = {"achieved_tflops": round(tf, 2), "peak_tflops": VALU_PEAK_TFLOPS,
@@ -218,6 +222,29 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(stage):
+    """HBM bytes per launch of the stage's kernel from the committed PMC
+    summary of this build (tools/pmc.sh -> profiles/pmc_current.txt):
+    (FETCH_SIZE + WRITE_SIZE) x 1 KiB.  Raw: the guide's x2 FETCH_SIZE
+    correction is calibrated for 16-B/lane streaming reads only, and these
+    kernels gather 48-B records (MI355X_MICROARCH.md, HBM)."""
+    path = os.path.join(ROOT, "profiles", "pmc_current.txt")
+    if not os.path.exists(path):
+        return None, None
+    want, cur, vals = "k_" + stage, None, {}
+    for line in open(path):
+        if line and not line[0].isspace():
+            cur = line.strip()
+        elif cur == want:
+            parts = line.split()
+            if len(parts) == 2:
+                vals[parts[0]] = float(parts[1])
+    if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
+        return None, None
+    return int((vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), \
+        "profiles/pmc_current.txt (rocprofv3 --pmc FETCH_SIZE + WRITE_SIZE, KiB, uncorrected)"
 
 
 def cpu_baseline(scene, W, H, cot, threads):
