@@ -66,17 +66,18 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) {
   return v < lo ? lo : (v > hi ? hi : v);
 }
 
-// expf for x in [-87, 88]: the same instruction sequence as ocml's expf
-// (Cody-Waite split of x*log2(e), v_exp_f32, ldexp) without its overflow /
-// underflow selects, which the blend never reaches (it only evaluates
-// exp(-s/2) for s <= 23.1).  Bit-identical to expf on that range.
+// exp(x) for the blend's range x in [-11.6, 0] (it evaluates exp(-s/2) only
+// for s <= 23.1): x*log2(e) split into ph + pl (Cody-Waite, as ocml's expf),
+// then 2^ph by v_exp_f32 corrected by (1 + pl ln2) -- no range reduction and
+// ldexp, since 2^ph stays a normal float here.  ~1 ulp, like expf; forward
+// and backward share it, so their decisions replay bit-identically (C3:
+// the same 9 knife-edge pixels vs the oracle as the full expf sequence).
 __device__ __forceinline__ float exp_inrange(float x) {
   const float ph = x * 0x1.715476p+0f;
   float pl = __builtin_fmaf(x, 0x1.715476p+0f, -ph);
   pl = __builtin_fmaf(x, 0x1.4ae0bep-26f, pl);
-  const float e = __builtin_rintf(ph);
-  const float a = (ph - e) + pl;
-  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(a), (int)e);
+  const float r = __builtin_amdgcn_exp2f(ph);
+  return __builtin_fmaf(r, pl * 0x1.62e430p-1f, r);
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
