@@ -80,6 +80,15 @@ __device__ __forceinline__ float exp_inrange(float x) {
   return __builtin_fmaf(r, pl * 0x1.62e430p-1f, r);
 }
 
+// s = [dx dy] Q [dx dy]^T for the blend's conic form (q00, qo = Q01+Q10,
+// q11) in the reference's unfused order (renderer.py:333).  A fused form
+// (5 operations instead of 8) was measured: with ill-conditioned conics the
+// cancellation amplifies its ~1-ulp difference into visible errors (needle
+// test: 1e-2 image error), so the reference's rounding is kept.
+__device__ __forceinline__ float conic_s(float dx, float dy, float q00, float qo, float q11) {
+  return ((dx * dx) * q00 + (qo * dx) * dy) + (dy * dy) * q11;
+}
+
 __device__ __forceinline__ unsigned long long lanemask_lt() {
   const int lane = threadIdx.x & (kWave - 1);
   return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -600,7 +609,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         const uint32_t j = 64u * wd + bit;
         const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
         const float dx = fx - pm.x, dy = fy - pm.y;
-        const float s = ((dx * dx) * pq.x + (pq.y * dx) * dy) + (dy * dy) * po.x;  // :333
+        const float s = conic_s(dx, dy, pq.x, pq.y, po.x);  // :333
         // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp
         const bool live = A < kAlphaStop && !(s > 23.1f);
         if (wave_any(live)) {
@@ -804,7 +813,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       const float2 pm = lds_pair(&s_rec[buf][6 * j]), pq = lds_pair(&s_rec[buf][6 * j + 1]),
                    po = lds_pair(&s_rec[buf][6 * j + 2]);
       const float dx = fx - pm.x, dy = fy - pm.y;
-      const float sq = ((dx * dx) * pq.x + (pq.y * dx) * dy) + (dy * dy) * po.x;
+      const float sq = conic_s(dx, dy, pq.x, pq.y, po.x);
       // exp(-11.55) < 1e-5: exact early skip (NaN falls through), as in the forward
       const bool live = (jbase + j < neval) && !(sq > 23.1f);
       if (wave_any(live)) {
@@ -846,23 +855,33 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       // pixel p = sub + 16k sits at (tile_x0 + 8((k>>2)&1) + (sub&7), tile_y0 + 8(k>>3) + 2(k&3) + (sub>>3))
       const float bx = (float)((tile % a.tiles_x) * GS_TILE + (sub & 7)) - mx;
       const float by = (float)((tile / a.tiles_x) * GS_TILE + (sub >> 3)) - my;
-      // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy) with Sx = sum ds dx, Sy = sum ds dy
-      float Sx = 0.f, Sy = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
+      // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy) with Sx = sum ds dx, Sy = sum ds dy.
+      // A lane's 16 pixels sit at (bx + ox_k, by + oy_k) with compile-time
+      // offsets ox_k in {0, 8}, oy_k in {0, 2, .., 14}: the sums over them of
+      // ds dx, ds dx^2, ds dx dy, .. are formed from sums of ds times the
+      // constant offsets (S0, Sox, Soxx, ..; zero offsets cost nothing), then
+      // expanded once per lane with bx, by.
+      float S0 = 0.f, Sox = 0.f, Soy = 0.f, Soxx = 0.f, Soxy = 0.f, Soyy = 0.f;
+      float g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
 #pragma unroll
       for (int kk = 0; kk < 16 / kRowsPerEntry; ++kk) {
         const int k = part + kRowsPerEntry * kk;
         const int p = sub + 16 * k;
         const float dop = s_dop[jj][p], cs = s_c[jj][p];
         const float4 pg = s_pg[p];
-        const float dx = bx + (float)(8 * ((k >> 2) & 1)), dy = by + (float)(8 * (k >> 3) + 2 * (k & 3));
+        const int ox = 8 * ((k >> 2) & 1), oy = 8 * (k >> 3) + 2 * (k & 3);
         const float cw = fabsf(cs);
         const float ds = cs > 0.f ? hop * dop : 0.f;
-        const float t = ds * dx, v = ds * dy;
-        Sx += t;
-        Sy += v;
-        g2 = __builtin_fmaf(t, dx, g2);
-        g3 = __builtin_fmaf(t, dy, g3);
-        g4 = __builtin_fmaf(v, dy, g4);
+        S0 += ds;
+        if (ox) {
+          Sox = __builtin_fmaf(ds, (float)ox, Sox);
+          Soxx = __builtin_fmaf(ds, (float)(ox * ox), Soxx);
+        }
+        if (oy) {
+          Soy = __builtin_fmaf(ds, (float)oy, Soy);
+          Soyy = __builtin_fmaf(ds, (float)(oy * oy), Soyy);
+        }
+        if (ox && oy) Soxy = __builtin_fmaf(ds, (float)(ox * oy), Soxy);
         g5 += dop;
         g6 = __builtin_fmaf(pg.x, cw, g6);
         g7 = __builtin_fmaf(pg.y, cw, g7);
@@ -872,6 +891,10 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         // of them needs > 128 VGPRs (fewer than 4 waves per SIMD)
         if (kk == 7) __builtin_amdgcn_sched_barrier(0);
       }
+      float Sx = __builtin_fmaf(bx, S0, Sox), Sy = __builtin_fmaf(by, S0, Soy);
+      float g2 = __builtin_fmaf(bx, __builtin_fmaf(bx, S0, 2.f * Sox), Soxx);
+      float g3 = __builtin_fmaf(bx, __builtin_fmaf(by, S0, Soy), __builtin_fmaf(by, Sox, Soxy));
+      float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
       Sx = row16_sum(Sx); Sy = row16_sum(Sy); g2 = row16_sum(g2); g3 = row16_sum(g3); g4 = row16_sum(g4);
       g5 = row16_sum(g5); g6 = row16_sum(g6); g7 = row16_sum(g7); g8 = row16_sum(g8); g9 = row16_sum(g9);
       if (kRowsPerEntry == 2) {  // rows 2i, 2i+1 of a wave hold halves of one entry

@@ -55,7 +55,8 @@ def main():
     qmax = qmax.permute(0, 2, 1, 3).reshape(ty_n * tx_n, 4)    # quadrant q = qx + 2 qy
     L = 23.1 * 1.001
     tot = {k: torch.zeros((), dtype=torch.long, device=dev)
-           for k in ("processed", "live", "bbox", "live_notbbox", "bwd_lockstep", "bwd_max", "bwd_sum")}
+           for k in ("processed", "live", "bbox", "live_notbbox", "bwd_lockstep", "bwd_max", "bwd_sum",
+                     "bwd_entries", "bwd_entries_live", "bwd_live_max", "bwd_live_sum")}
     ys, xs = torch.meshgrid(torch.arange(8, device=dev), torch.arange(8, device=dev), indexing="ij")
     ys, xs = ys.reshape(-1).float(), xs.reshape(-1).float()
     num_tiles = tx_n * ty_n
@@ -102,10 +103,27 @@ def main():
                 tot["bwd_lockstep"] += 4 * stop
                 tot["bwd_max"] += (4 * per.max(1).values).sum().long()
                 tot["bwd_sum"] += per.sum().long()
+                # exact liveness (what the forward's bitmap holds), and batches
+                # formed from entries with at least one live quadrant
+                lv = live[:stop]
+                anyq = lv.any(1)
+                tot["bwd_entries"] += stop
+                tot["bwd_entries_live"] += anyq.sum()
+                lvc = lv[anyq].float()
+                nl = lvc.shape[0]
+                if nl:
+                    nb2 = (nl + 15) // 16
+                    lpad = torch.zeros(nb2 * 16, 4, device=dev)
+                    lpad[:nl] = lvc
+                    per2 = lpad.view(nb2, 16, 4).sum(1)
+                    tot["bwd_live_max"] += (4 * per2.max(1).values).sum().long()
+                    tot["bwd_live_sum"] += per2.sum().long()
     tot = {k: int(v) for k, v in tot.items()}
     print(tot)
     print(f"backward phase-A wave-entries: lockstep {tot['bwd_lockstep']}, culled+barrier {tot['bwd_max']}, "
           f"decoupled {tot['bwd_sum']}")
+    print(f"backward entries up to the tile stop {tot['bwd_entries']}, with a live quadrant {tot['bwd_entries_live']}; "
+          f"compacted batches: busiest-wave {tot['bwd_live_max']}, decoupled {tot['bwd_live_sum']}")
     p = tot["processed"]
     print(f"live/processed = {tot['live'] / p:.3f}, bbox/processed = {tot['bbox'] / p:.3f}, "
           f"evaluated pairs (E) = {int(neval.sum())}, processed lane-pairs = {64 * p}")
