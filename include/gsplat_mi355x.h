@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2
+#define GS_ABI_VERSION 3
 #define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_MAX_RECT_TILES 8   /* r <= 50 px -> an AABB spans at most 8 tiles per axis */
@@ -79,6 +79,9 @@ typedef struct gs_gaussians {
   int64_t color_stride;
   const float *opacity;      /* [n, opacity_stride] get_opacity.squeeze(1) as given (renderer.py:94) */
   int64_t opacity_stride;
+  int32_t opacity_is_logit;  /* 1: opacity holds the model's raw _opacity; the kernels apply
+                                get_opacity's sigmoid (gaussian_model.py:119-120) and d_opacity
+                                is the gradient w.r.t. the logit */
 } gs_gaussians;
 
 /* ---- Stage 1: _project_gaussians_3d_to_2d + _frustum_culling ----------

@@ -24,7 +24,7 @@ GS_TILE = 16
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 2
+GS_ABI_VERSION = 3
 
 _vp = C.c_void_p
 
@@ -42,7 +42,7 @@ class GsGaussians(C.Structure):
     _fields_ = [
         ("n", C.c_int32), ("xyz", _vp), ("xyz_stride", C.c_int64), ("cov3d", _vp),
         ("scaling", _vp), ("rotation", _vp), ("color_logits", _vp), ("color_stride", C.c_int64),
-        ("opacity", _vp), ("opacity_stride", C.c_int64),
+        ("opacity", _vp), ("opacity_stride", C.c_int64), ("opacity_is_logit", C.c_int32),
     ]
 
 

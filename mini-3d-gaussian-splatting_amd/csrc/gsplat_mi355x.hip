@@ -254,7 +254,8 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
         rinfo = (uint32_t)(x0 / T) | ((uint32_t)(y0 / T) << 12) | ((uint32_t)((x1 - 1) / T - x0 / T) << 24);
       }
       const float *cl = a.g.color_logits + (int64_t)g * a.g.color_stride;
-      const float op = a.g.opacity[(int64_t)g * a.g.opacity_stride];
+      float op = a.g.opacity[(int64_t)g * a.g.opacity_stride];
+      if (a.g.opacity_is_logit) op = 1.f / (1.f + expf(-op));  // get_opacity
       float4 *rec = reinterpret_cast<float4 *>(a.records) + 3 * (int64_t)g;
       // record: mx my q00 qo | q11 o r g | b z off rinfo  (read as 8-byte pairs by the blend)
       const float cr = 1.f / (1.f + expf(-cl[0])), cg = 1.f / (1.f + expf(-cl[1])), cb = 1.f / (1.f + expf(-cl[2]));  // sigmoid (:90)
@@ -987,7 +988,12 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
     const float c = 1.f / (1.f + expf(-cl[k]));
     a.d_color_logits[3 * (size_t)g + k] = acc[6 + k] * c * (1.f - c);
   }
-  a.d_opacity[g] = acc[5];
+  float dop = acc[5];
+  if (a.g.opacity_is_logit) {  // through get_opacity's sigmoid, as torch's sigmoid_backward
+    const float o = 1.f / (1.f + expf(-a.g.opacity[(int64_t)g * a.g.opacity_stride]));
+    dop = (dop * (1.f - o)) * o;
+  }
+  a.d_opacity[g] = dop;
   const bool any = dm0 != 0.0 || dm1 != 0.0 || G[0] != 0.0 || G[1] != 0.0 || G[2] != 0.0 ||
                    G[3] != 0.0 || acc[9] != 0.f;
   const bool raw = a.g.cov3d == nullptr;

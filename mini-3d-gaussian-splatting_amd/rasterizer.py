@@ -68,7 +68,7 @@ def _rows(t: torch.Tensor, cols: int) -> Tuple[torch.Tensor, int]:
     return t, t.stride(0)
 
 
-def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity) -> N.GsGaussians:
+def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False) -> N.GsGaussians:
     g = N.GsGaussians()
     g.n = n
     g.xyz, g.xyz_stride = N.ptr(xyz), xyz.stride(0)
@@ -76,6 +76,7 @@ def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity) -> N.Gs
     g.scaling, g.rotation = N.ptr(scaling), N.ptr(rotation)
     g.color_logits, g.color_stride = N.ptr(logits), logits.stride(0)
     g.opacity, g.opacity_stride = N.ptr(opacity), opacity.stride(0)
+    g.opacity_is_logit = 1 if opacity_is_logit else 0
     return g
 
 
@@ -88,11 +89,12 @@ class StageTimer:
     launched on (torch's current stream).  Disabled unless a bench enables it;
     when disabled, mark() is a no-op."""
     enabled = False
+    only = None  # optional set of stage names to record (the others cost nothing)
     events: list = []
 
     @classmethod
     def mark(cls, name: str):
-        if cls.enabled:
+        if cls.enabled and (cls.only is None or name in cls.only):
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             cls.events.append((name, e))
@@ -123,10 +125,10 @@ def _check_inputs(xyz: torch.Tensor):
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
     __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_acc",
-                 "pix_state", "live_bits", "M", "T")
+                 "pix_state", "live_bits", "big", "M", "T")
 
 
-def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity):
+def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False):
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -134,7 +136,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     f32, i32 = torch.float32, torch.int32
     s = _stream()
     cs = cam.to_struct()
-    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity)
+    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit)
 
     means2d = torch.empty((n, 2), dtype=f32, device=dev)
     conics = torch.empty((n, 2, 2), dtype=f32, device=dev)
@@ -166,6 +168,16 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
                          N.ptr(counters), N.ptr(bws), bws.numel(), 0, 0, 0, N.ptr(records))
         StageTimer.mark("bin_count")
         N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
+        # everything whose size does not depend on T is allocated before the
+        # one host sync, so the GPU waits only for the read-back and launches
+        num_tiles = cam.tiles_x * cam.tiles_y
+        pair_offset = torch.empty((n,), dtype=i32, device=dev)
+        ranges = torch.empty((num_tiles, 2), dtype=i32, device=dev)
+        image = torch.empty((3, H, W), dtype=f32, device=dev)
+        alpha = torch.empty((1, H, W), dtype=f32, device=dev)
+        depth = torch.empty((1, H, W), dtype=f32, device=dev)
+        pix_acc = torch.empty((H * W, 4), dtype=f32, device=dev)
+        pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
         StageTimer.mark("~sync")
         M, T = (int(v) for v in counters[:2].tolist())  # the one host sync
     else:
@@ -181,47 +193,53 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         fr.pair_offset = torch.zeros((max(n, 1),), dtype=i32, device=dev)
         return image, alpha, depth, means2d, conics, radii, vis, fr
 
-    num_tiles = cam.tiles_x * cam.tiles_y
-    tk = torch.empty((2, T), dtype=i32, device=dev)
-    tv = torch.empty((2, T), dtype=i32, device=dev)  # values = Gaussian ids
-    pair_offset = torch.empty((n,), dtype=i32, device=dev)
-    ba.tile_keys, ba.pair_gauss, ba.pair_offset = N.ptr(tk[0]), N.ptr(tv[0]), N.ptr(pair_offset)
+    # The T-sized buffers in one allocation, addressed by pointer arithmetic:
+    # between the host sync and the blend launch the GPU idles, so this span
+    # does no torch work beyond the allocation (tensor views of the sorted ids
+    # and the bitmap are made after the blend is queued).
+    tws_bytes = int(lib.gs_radix_sort_workspace_bytes(T))
+    live_words = int(lib.gs_blend_live_words(T, num_tiles))
+    sizes = (4 * T * 4, tws_bytes, 4 * live_words * 8)
+    offs = [0]
+    for sz in sizes:
+        offs.append(offs[-1] + (sz + 255) // 256 * 256)
+    big = torch.empty((offs[-1],), dtype=torch.uint8, device=dev)
+    base = big.data_ptr()
+    p_tk = (base, base + 4 * T)                  # tile keys, ping-pong
+    p_tv = (base + 8 * T, base + 12 * T)         # Gaussian ids, ping-pong
+    p_ws, p_live = base + offs[1], base + offs[2]
+    ba.tile_keys, ba.pair_gauss, ba.pair_offset = p_tk[0], p_tv[0], N.ptr(pair_offset)
     StageTimer.mark("bin_emit")
     N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
 
     bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
-    tws = torch.empty((lib.gs_radix_sort_workspace_bytes(T),), dtype=torch.uint8, device=dev)
     alt = C.c_int32(0)
     StageTimer.mark("tile_sort")
-    N.check(lib.gs_radix_sort_pairs(N.ptr(tk[0]), N.ptr(tv[0]), N.ptr(tk[1]), N.ptr(tv[1]), T, 0, bits, 0,
-                                    N.ptr(tws), tws.numel(), C.byref(alt), s), "tile sort")
-    sorted_keys, sorted_gauss = tk[alt.value], tv[alt.value]
-    ranges = torch.empty((num_tiles, 2), dtype=i32, device=dev)
-    ra = N.GsRangeArgs(T, num_tiles, N.ptr(sorted_keys), N.ptr(ranges))
+    N.check(lib.gs_radix_sort_pairs(p_tk[0], p_tv[0], p_tk[1], p_tv[1], T, 0, bits, 0,
+                                    p_ws, tws_bytes, C.byref(alt), s), "tile sort")
+    ra = N.GsRangeArgs(T, num_tiles, p_tk[alt.value], N.ptr(ranges))
     StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
-    image = torch.empty((3, H, W), dtype=f32, device=dev)
-    alpha = torch.empty((1, H, W), dtype=f32, device=dev)
-    depth = torch.empty((1, H, W), dtype=f32, device=dev)
-    pix_acc = torch.empty((H * W, 4), dtype=f32, device=dev)
-    pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
-    live_words = int(lib.gs_blend_live_words(T, num_tiles))
-    live_bits = torch.empty((4, live_words), dtype=torch.int64, device=dev)
-    fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), N.ptr(sorted_gauss), N.ptr(records),
+    fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), p_tv[alt.value], N.ptr(records),
                           N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state),
-                          N.ptr(live_bits), live_words)
+                          p_live, live_words)
     StageTimer.mark("blend_fwd")
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
     StageTimer.mark("~end_fwd")
 
-    fr.pair_offset, fr.ranges, fr.sorted_gauss = pair_offset, ranges, sorted_gauss
-    fr.pix_acc, fr.pix_state, fr.live_bits = pix_acc, pix_state, live_bits
+    # (the blend is queued: views for the frame cost no GPU idle time now)
+    kv = big[:sizes[0]].view(i32).view(4, T)
+    fr.sorted_gauss = kv[2 + alt.value]
+    fr.live_bits = big[offs[2]:offs[2] + sizes[2]].view(torch.int64).view(4, live_words)
+    fr.big = big
+    fr.pair_offset, fr.ranges = pair_offset, ranges
+    fr.pix_acc, fr.pix_state = pix_acc, pix_state
     return image, alpha, depth, means2d, conics, radii, vis, fr
 
 
 def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotation, logits, opacity,
-                      means2d, conics, g_image, g_alpha, g_depth, g_means2d, g_conics):
+                      means2d, conics, g_image, g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit=False):
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -252,7 +270,7 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     d_op = torch.empty((n,), dtype=f32, device=dev)
     gm = None if g_means2d is None else g_means2d.contiguous()
     gc = None if g_conics is None else g_conics.contiguous()
-    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity)
+    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit)
     pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
                             # Gaussian order (order=NULL): inputs/outputs stream; walking in depth
                             # order coalesces the slot reads but scatters 10 arrays (measured 2.4x slower)
@@ -269,10 +287,10 @@ class RasterizeGaussians(torch.autograd.Function):
     are (image, alpha, depth, viewspace_points, conics, radii, visibility)."""
 
     @staticmethod
-    def forward(ctx, xyz, cov3d, scaling, rotation, logits, opacity, cam: CameraParams):
+    def forward(ctx, xyz, cov3d, scaling, rotation, logits, opacity, cam: CameraParams, opacity_is_logit=False):
         image, alpha, depth, means2d, conics, radii, vis, fr = forward_pipeline(
-            cam, xyz, cov3d, scaling, rotation, logits, opacity)
-        ctx.cam, ctx.frame = cam, fr
+            cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit)
+        ctx.cam, ctx.frame, ctx.opacity_is_logit = cam, fr, opacity_is_logit
         ctx.save_for_backward(xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics)
         ctx.mark_non_differentiable(radii, vis)
         ctx.set_materialize_grads(False)
@@ -284,7 +302,7 @@ class RasterizeGaussians(torch.autograd.Function):
         g_conics = None if g_conics is None else g_conics.reshape(-1, 4)
         d_xyz, d_cov, d_scl, d_rot, d_col, d_op = backward_pipeline(
             ctx.cam, ctx.frame, xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics,
-            g_image, None if g_alpha is None else g_alpha, g_depth, g_means2d, g_conics)
+            g_image, None if g_alpha is None else g_alpha, g_depth, g_means2d, g_conics, ctx.opacity_is_logit)
         need = ctx.needs_input_grad
         return (d_xyz if need[0] else None,
                 d_cov if (cov3d is not None and need[1]) else None,
@@ -292,10 +310,12 @@ class RasterizeGaussians(torch.autograd.Function):
                 d_rot if (rotation is not None and need[3]) else None,
                 d_col if need[4] else None,
                 d_op.view(opacity.shape) if need[5] else None,
-                None)
+                None, None)
 
 
-def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity):
+def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False):
+    """opacity_is_logit: opacity holds the model's raw _opacity and the kernels
+    apply get_opacity's sigmoid (fused; its gradient goes to the logit)."""
     _check_inputs(xyz)
     if cov3d is not None:
         cov3d = cov3d.reshape(-1, 3, 3)
@@ -307,4 +327,4 @@ def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity)
     xyz, _ = _rows(xyz, 3)
     logits, _ = _rows(logits, 3)
     opacity, _ = _rows(opacity, 1)
-    return RasterizeGaussians.apply(xyz, cov3d, scaling, rotation, logits, opacity, cam)
+    return RasterizeGaussians.apply(xyz, cov3d, scaling, rotation, logits, opacity, cam, bool(opacity_is_logit))

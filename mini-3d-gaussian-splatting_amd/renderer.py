@@ -77,9 +77,14 @@ class GaussianRenderer:
     def render(self, camera, gaussians, settings: RenderSettings) -> Dict[str, torch.Tensor]:
         cam = camera_params(camera, settings, self.radius_min, self.radius_max)
         xyz = gaussians.get_xyz
-        if getattr(gaussians, "_gs_fused_covariance", False):
+        fused = getattr(gaussians, "_gs_fused_covariance", False)
+        if fused:
+            # this package's GaussianModel: covariance from the raw scaling /
+            # rotation and get_opacity's sigmoid are computed in the kernels;
+            # squeeze (a view) keeps autograd from materialising a zero-filled
+            # [N,1,3] gradient as a select would
             cov3d, scaling, rotation = None, gaussians._scaling, gaussians._rotation
-            logits = gaussians._features_dc[:, 0, :]
+            logits = gaussians._features_dc.squeeze(1)
         else:
             cov3d, scaling, rotation = gaussians.get_covariance, None, None
             feats = gaussians.get_features
@@ -87,9 +92,9 @@ class GaussianRenderer:
                 logits = feats[:, 0, :]
             else:
                 logits = gaussians._features_dc.squeeze(1)
-        opacity = gaussians.get_opacity.squeeze(1)
+        opacity = gaussians._opacity.squeeze(1) if fused else gaussians.get_opacity.squeeze(1)
         image, alpha, depth, means2d, conics, radii, vis = rasterize(
-            cam, xyz, cov3d, scaling, rotation, logits, opacity)
+            cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=fused)
         return {
             "image": image,
             "alpha": alpha,
