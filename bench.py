@@ -201,7 +201,7 @@ def main():
         # alpha / colour / depth gradient 20, the 10 per-pair sums 20)
         flops_fwd, flops_bwd = 26 * E, 66 * E
         kern = {"blend_fwd": (bytes_fwd, flops_fwd), "blend_bwd": (bytes_bwd, flops_bwd)}
-        dom = max((k for k in kern if k in stages), key=lambda k: stages[k])
+        dom = max((k for k in kern if k in stages), key=lambda k: stages[k]) if stages else "blend_bwd"
         # the dominant kernel's average launch, measured live in the timed region
         t_ms = sum(bwd_live) / len(bwd_live) if dom == "blend_bwd" and bwd_live else stages[dom]
         ach = kern[dom][0] / (t_ms * 1e-3) / 1e9

@@ -478,12 +478,22 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   }
 }
 
+// Every tile's [start, end) from the tile-sorted keys, empty tiles included
+// (no memset): position p in [0, T] is a boundary when key[p-1] != key[p]
+// (key[-1] = -1, key[T] = num_tiles); it closes the previous tile, opens the
+// next and writes the tiles in between as empty at p.
 __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
   const long long p = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (p >= a.num_pairs) return;
-  const uint32_t t = a.sorted_keys[p];
-  if (p == 0 || a.sorted_keys[p - 1] != t) a.ranges[2 * t] = (uint32_t)p;
-  if (p == a.num_pairs - 1 || a.sorted_keys[p + 1] != t) a.ranges[2 * t + 1] = (uint32_t)(p + 1);
+  if (p > a.num_pairs) return;
+  const long long prev = p > 0 ? (long long)a.sorted_keys[p - 1] : -1;
+  const long long cur = p < a.num_pairs ? (long long)a.sorted_keys[p] : (long long)a.num_tiles;
+  if (cur == prev) return;
+  if (prev >= 0) a.ranges[2 * prev + 1] = (uint32_t)p;
+  for (long long t = prev + 1; t < cur; ++t) {
+    a.ranges[2 * t] = (uint32_t)p;
+    a.ranges[2 * t + 1] = (uint32_t)p;
+  }
+  if (cur < a.num_tiles) a.ranges[2 * cur] = (uint32_t)p;
 }
 
 // ======================================================== blend fwd =======
@@ -1291,11 +1301,10 @@ gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream) {
 gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream) {
   if (!a || !a->ranges) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_tile_ranges");
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(a->ranges, 0, sizeof(uint32_t) * 2 * (size_t)a->num_tiles, s) != hipSuccess)
-    return fail(GS_ERR_LAUNCH, "%s: memset failed", "gs_tile_ranges");
-  if (a->num_pairs <= 0) return GS_OK;
-  if (!a->sorted_keys) return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_ranges");
-  k_tile_ranges<<<div_up(a->num_pairs, kBlock), kBlock, 0, s>>>(*a);
+  if (a->num_pairs < 0 || a->num_tiles < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative size", "gs_tile_ranges");
+  if (a->num_tiles == 0) return GS_OK;
+  if (a->num_pairs > 0 && !a->sorted_keys) return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_ranges");
+  k_tile_ranges<<<div_up(a->num_pairs + 1, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_tile_ranges");
 }
 

@@ -128,6 +128,19 @@ class _Frame:
                  "pix_state", "live_bits", "big", "M", "T")
 
 
+_T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess)
+
+
+def _alloc_tile_buffers(lib, cap: int, num_tiles: int, dev):
+    """One byte buffer for T <= cap entries: tile keys + Gaussian ids
+    (ping-pong, 16 B/entry), the tile sort's workspace and the liveness
+    bitmap (4 x gs_blend_live_words)."""
+    nbytes = (16 * cap + 255) // 256 * 256
+    nbytes += (int(lib.gs_radix_sort_workspace_bytes(cap)) + 255) // 256 * 256
+    nbytes += 32 * int(lib.gs_blend_live_words(cap, num_tiles))
+    return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
+
+
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False):
     lib = N.load()
     dev = xyz.device
@@ -178,8 +191,13 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         depth = torch.empty((1, H, W), dtype=f32, device=dev)
         pix_acc = torch.empty((H * W, 4), dtype=f32, device=dev)
         pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
+        # the T-sized buffers too, at a capacity guessed from the last frame on
+        # this device (re-allocated after the sync if T exceeds it)
+        cap = _T_SEEN.get(dev, 0)
+        big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, dev) if cap else None
         StageTimer.mark("~sync")
         M, T = (int(v) for v in counters[:2].tolist())  # the one host sync
+        _T_SEEN[dev] = T
     else:
         M, T = 0, 0
     fr.M, fr.T = M, T
@@ -193,21 +211,19 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         fr.pair_offset = torch.zeros((max(n, 1),), dtype=i32, device=dev)
         return image, alpha, depth, means2d, conics, radii, vis, fr
 
-    # The T-sized buffers in one allocation, addressed by pointer arithmetic:
-    # between the host sync and the blend launch the GPU idles, so this span
-    # does no torch work beyond the allocation (tensor views of the sorted ids
-    # and the bitmap are made after the blend is queued).
+    # The T-sized buffers live in one allocation addressed by pointer
+    # arithmetic: between the host sync and the blend launch the GPU idles,
+    # so this span does no torch work (views of the sorted ids and the bitmap
+    # are made after the blend is queued).
+    big, cap_t = big_guess if big_guess is not None and big_guess[1] >= T else _alloc_tile_buffers(lib, T, num_tiles, dev)
     tws_bytes = int(lib.gs_radix_sort_workspace_bytes(T))
     live_words = int(lib.gs_blend_live_words(T, num_tiles))
-    sizes = (4 * T * 4, tws_bytes, 4 * live_words * 8)
-    offs = [0]
-    for sz in sizes:
-        offs.append(offs[-1] + (sz + 255) // 256 * 256)
-    big = torch.empty((offs[-1],), dtype=torch.uint8, device=dev)
     base = big.data_ptr()
-    p_tk = (base, base + 4 * T)                  # tile keys, ping-pong
-    p_tv = (base + 8 * T, base + 12 * T)         # Gaussian ids, ping-pong
-    p_ws, p_live = base + offs[1], base + offs[2]
+    p_tk = (base, base + 4 * cap_t)                   # tile keys, ping-pong
+    p_tv = (base + 8 * cap_t, base + 12 * cap_t)      # Gaussian ids, ping-pong
+    o_ws = (16 * cap_t + 255) // 256 * 256
+    o_live = o_ws + (int(lib.gs_radix_sort_workspace_bytes(cap_t)) + 255) // 256 * 256
+    p_ws, p_live = base + o_ws, base + o_live
     ba.tile_keys, ba.pair_gauss, ba.pair_offset = p_tk[0], p_tv[0], N.ptr(pair_offset)
     StageTimer.mark("bin_emit")
     N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
@@ -229,9 +245,9 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     StageTimer.mark("~end_fwd")
 
     # (the blend is queued: views for the frame cost no GPU idle time now)
-    kv = big[:sizes[0]].view(i32).view(4, T)
-    fr.sorted_gauss = kv[2 + alt.value]
-    fr.live_bits = big[offs[2]:offs[2] + sizes[2]].view(torch.int64).view(4, live_words)
+    kv = big[:16 * cap_t].view(i32).view(4, cap_t)
+    fr.sorted_gauss = kv[2 + alt.value, :T]
+    fr.live_bits = big[o_live:o_live + 32 * live_words].view(torch.int64).view(4, live_words)
     fr.big = big
     fr.pair_offset, fr.ranges = pair_offset, ranges
     fr.pix_acc, fr.pix_state = pix_acc, pix_state

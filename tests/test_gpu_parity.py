@@ -215,6 +215,26 @@ def test_radix_sort_matches_stable_argsort(pkg, cuda):
         assert np.array_equal(kk[alt.value].cpu().numpy().view(np.uint32), k[order])
 
 
+def test_tile_ranges_every_tile(pkg, cuda):
+    """gs_tile_ranges writes every tile, empty ones as [p, p) (no memset), and
+    all-empty lists."""
+    import ctypes as C
+    N = pkg._native
+    lib = N.load()
+    stream = torch.cuda.current_stream().cuda_stream
+    for keys, ntiles in (([2, 2, 5, 5, 5, 9], 12), ([0, 0, 1], 2), ([], 7), ([3], 4)):
+        k = torch.tensor(keys if keys else [0], dtype=torch.int32, device=cuda)
+        ranges = torch.full((ntiles, 2), -7, dtype=torch.int32, device=cuda)
+        ra = N.GsRangeArgs(len(keys), ntiles, N.ptr(k), N.ptr(ranges))
+        N.check(lib.gs_tile_ranges(C.byref(ra), stream), "gs_tile_ranges")
+        want = []
+        for t in range(ntiles):
+            lo = sum(1 for v in keys if v < t)
+            hi = sum(1 for v in keys if v <= t)
+            want.append((lo, hi))
+        assert ranges.cpu().tolist() == [list(w) for w in want], (keys, ranges.cpu().tolist())
+
+
 def test_deterministic(pkg, cuda):
     """No float atomics anywhere: two runs are bit-identical, grads included."""
     syn = pkg.synthetic
