@@ -260,6 +260,33 @@ typedef struct gs_adam_args {
 } gs_adam_args;
 gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream);
 
+/* ---- Photometric loss ---------------------------------
+ * total = (1 - lambda) * L1 + lambda * D-SSIM, the objective of GaussianLoss
+ * (src/core/loss.py:41-63): L1 = mean |pred - target| (:56); D-SSIM =
+ * 1 - mean(clamp(SSIM map, 0, 1)) over the statistics SSIMLoss builds
+ * (:17-39): a K-tap Gaussian window with sigma = K/6, separable, zero
+ * padding, C1 = 0.01^2, C2 = 0.03^2.  The reference SSIMLoss.forward ends
+ * without a return; its caller consumes the value as `dssim` (:57-58), which
+ * is the D-SSIM form implemented here.  Deterministic (fixed-order
+ * reductions, no atomics). */
+#define GS_LOSS_MAX_WINDOW 11
+typedef struct gs_loss_args {
+  int32_t channels, height, width; /* pred/target/d_pred: [C,H,W] fp32 contiguous */
+  const float *pred, *target;
+  float lambda_dssim;                /* loss.py:42 default 0.2 */
+  int32_t window;                    /* odd, 1..GS_LOSS_MAX_WINDOW (loss.py:10 default 11) */
+  float c1, c2;                      /* loss.py:14-15 */
+  void *workspace;                   /* gs_loss_workspace_bytes */
+  size_t workspace_bytes;
+  float *maps;                       /* [3,C,H,W] written by the forward for the backward, or NULL */
+  float *out;                        /* [3] total, l1, dssim (device) */
+  const float *g_total;              /* backward: dL/dtotal (device scalar), NULL = 1 */
+  float *d_pred;                     /* backward: [C,H,W] */
+} gs_loss_args;
+size_t gs_loss_workspace_bytes(int32_t channels, int32_t height, int32_t width);
+gs_status gs_loss_forward(const gs_loss_args *a, gs_stream_t stream);
+gs_status gs_loss_backward(const gs_loss_args *a, gs_stream_t stream);
+
 /* ---- misc --------------------------------------------------------------- */
 int32_t gs_abi_version(void);
 const char *gs_last_error(void);

@@ -9,7 +9,8 @@ from .renderer import GaussianRenderer, RenderSettings, camera_params  # noqa: F
 from .gaussian_model import GaussianModel, build_rotation_matrix  # noqa: F401
 from .camera import Camera, CameraUtils  # noqa: F401
 from .rasterizer import CameraParams, rasterize  # noqa: F401
-from . import _native, synthetic, distributed, optim  # noqa: F401
+from .loss import SSIMLoss, GaussianLoss, photometric_loss  # noqa: F401
+from . import _native, synthetic, distributed, optim, loss  # noqa: F401
 
 __all__ = ["GaussianRenderer", "RenderSettings", "GaussianModel", "Camera", "CameraUtils",
-           "CameraParams", "rasterize", "camera_params"]
+           "CameraParams", "rasterize", "camera_params", "SSIMLoss", "GaussianLoss", "photometric_loss"]

@@ -110,12 +110,24 @@ class GsAdamArgs(C.Structure):
     ]
 
 
+GS_LOSS_MAX_WINDOW = 11
+
+
+class GsLossArgs(C.Structure):
+    _fields_ = [
+        ("channels", C.c_int32), ("height", C.c_int32), ("width", C.c_int32), ("pred", _vp), ("target", _vp),
+        ("lambda_dssim", C.c_float), ("window", C.c_int32), ("c1", C.c_float), ("c2", C.c_float),
+        ("workspace", _vp), ("workspace_bytes", C.c_size_t), ("maps", _vp), ("out", _vp), ("g_total", _vp),
+        ("d_pred", _vp),
+    ]
+
+
 # Every symbol the header declares (checked by tests/test_abi.py).
 EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
     "gs_tile_ranges", "gs_blend_live_words", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-    "gs_adam_step",
+    "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
 )
 
 _lib = None
@@ -146,9 +158,13 @@ def _declare(lib):
     lib.gs_blend_backward.argtypes = [P(GsBlendBwdArgs), _vp]
     lib.gs_project_backward.argtypes = [P(GsProjectBwdArgs), _vp]
     lib.gs_adam_step.argtypes = [P(GsAdamArgs), _vp]
+    lib.gs_loss_workspace_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    lib.gs_loss_workspace_bytes.restype = C.c_size_t
+    lib.gs_loss_forward.argtypes = [P(GsLossArgs), _vp]
+    lib.gs_loss_backward.argtypes = [P(GsLossArgs), _vp]
     for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_bin_count", "gs_bin_emit",
               "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-              "gs_adam_step"):
+              "gs_adam_step", "gs_loss_forward", "gs_loss_backward"):
         getattr(lib, f).restype = C.c_int
 
 

@@ -13,8 +13,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", "gsplat_mi355x.hip")]
-HDR = [os.path.join(ROOT, "include", "gsplat_mi355x.h")]
+SRC = [os.path.join(HERE, "csrc", "gsplat_mi355x.hip"), os.path.join(HERE, "csrc", "gs_loss.hip")]
+HDR = [os.path.join(ROOT, "include", "gsplat_mi355x.h"), os.path.join(HERE, "csrc", "gs_internal.h")]
 OUT = os.path.join(HERE, "libgsplat_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",

@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include "gsplat_mi355x.h"
+#include "gs_internal.h"
 
 namespace {
 
@@ -1205,6 +1206,9 @@ bool cam_ok(const gs_camera &c) {
 }
 
 }  // namespace
+
+gs_status gs_internal_fail(gs_status s, const char *fmt, const char *what) { return fail(s, fmt, what); }
+gs_status gs_internal_check_launch(const char *what) { return check_launch(what); }
 
 // ============================================================ C ABI =======
 extern "C" {

@@ -38,7 +38,7 @@ def test_abi_version(pkg):
 def test_struct_layouts_match_c(pkg, tmp_path):
     N = pkg._native
     names = ["gs_camera", "gs_gaussians", "gs_project_args", "gs_bin_args", "gs_range_args",
-             "gs_blend_fwd_args", "gs_blend_bwd_args", "gs_project_bwd_args"]
+             "gs_blend_fwd_args", "gs_blend_bwd_args", "gs_project_bwd_args", "gs_adam_args", "gs_loss_args"]
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "gsplat_mi355x.h"\nint main(){' +
                    "".join('printf("%%zu\\n", sizeof(%s));' % n for n in names) + "}")
@@ -46,7 +46,8 @@ def test_struct_layouts_match_c(pkg, tmp_path):
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     sizes = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     py = [C.sizeof(t) for t in (N.GsCamera, N.GsGaussians, N.GsProjectArgs, N.GsBinArgs, N.GsRangeArgs,
-                                N.GsBlendFwdArgs, N.GsBlendBwdArgs, N.GsProjectBwdArgs)]
+                                N.GsBlendFwdArgs, N.GsBlendBwdArgs, N.GsProjectBwdArgs, N.GsAdamArgs,
+                                N.GsLossArgs)]
     assert sizes == py
 
 
@@ -63,6 +64,20 @@ def test_bad_arguments_are_reported(pkg):
     assert lib.gs_project_forward(C.byref(a), None) == 3  # unsupported tile size
     with pytest.raises(RuntimeError, match="gs_status=3"):
         N.check(lib.gs_project_forward(C.byref(a), None), "gs_project_forward")
+
+
+def test_loss_bad_arguments(pkg):
+    N = pkg._native
+    lib = N.load()
+    assert lib.gs_loss_forward(None, None) == 1
+    a = N.GsLossArgs(channels=3, height=8, width=8, window=10)
+    assert lib.gs_loss_forward(C.byref(a), None) == 3  # even window
+    a.window = 11
+    assert lib.gs_loss_forward(C.byref(a), None) == 1  # null buffers
+    assert b"gs_loss_forward" in lib.gs_last_error()
+    assert lib.gs_loss_backward(C.byref(a), None) == 1
+    assert lib.gs_loss_workspace_bytes(3, 1080, 1920) == 8 * 3 * 68 * 120
+    assert lib.gs_loss_workspace_bytes(0, 4, 4) == 0
 
 
 def test_workspace_queries(pkg):
