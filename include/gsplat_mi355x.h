@@ -287,6 +287,54 @@ size_t gs_loss_workspace_bytes(int32_t channels, int32_t height, int32_t width);
 gs_status gs_loss_forward(const gs_loss_args *a, gs_stream_t stream);
 gs_status gs_loss_backward(const gs_loss_args *a, gs_stream_t stream);
 
+/* ---- Densification ------------------------------------
+ * One pass of split / clone / prune over the model's raw parameters
+ * (gaussian_model.py:130-175 density_and_split / density_and_clone,
+ * optimizer.py:64-66 opacity prune), with the Adam moments remapped: kept
+ * Gaussians carry theirs, new ones start at zero.  Per Gaussian i, on the
+ * pre-densify state: g = |dL/dxyz_i|, s = mean(exp(scaling_i));
+ *   split = g > grad_threshold and s > split_size * scene_extent (:137):
+ *     i is replaced by two children xyz -/+ R(q)[:,0] * 0.5 s, scaling
+ *     log(0.75 exp(scaling)), rotation normalize(q), opacity
+ *     clamp(logit(sigmoid(op)), -6, 6), features copied (:139-154);
+ *   clone = g > grad_threshold and s < clone_size * scene_extent (:166):
+ *     i stays and a copy is added at xyz + N(0,1)^3 * 0.5 s (:169-178);
+ *   prune: every output whose sigmoid(opacity) <= min_opacity is dropped.
+ * Output order: kept originals, split "-" children, split "+" children,
+ * clones; each in the original index order.  (The reference cannot run
+ * these: _append_points reads a missing `_scaling_log` (:229).)  Two
+ * phases: gs_densify_count writes counters, the caller sizes the outputs. */
+#define GS_DENSIFY_SPLIT 1
+#define GS_DENSIFY_CLONE 2
+#define GS_DENSIFY_PRUNE 4
+typedef struct gs_model_arrays {
+  float *xyz;           /* [n,3]   _xyz */
+  float *features_dc;   /* [n,3]   _features_dc */
+  float *features_rest; /* [n,rest_floats] _features_rest */
+  float *scaling;       /* [n,3]   _scaling (log) */
+  float *rotation;      /* [n,4]   _rotation */
+  float *opacity;       /* [n]     _opacity (logit) */
+} gs_model_arrays;
+typedef struct gs_densify_args {
+  int32_t n;
+  int32_t rest_floats;
+  gs_model_arrays in;             /* read only */
+  const float *xyz_grad;          /* [n,3], or NULL: nothing is split or cloned */
+  float grad_threshold, scene_extent;
+  float split_size, clone_size;   /* 0.03, 0.01 (gaussian_model.py:137,166) */
+  float min_opacity;              /* 0.01 (optimizer.py:64) */
+  int32_t flags;                  /* GS_DENSIFY_SPLIT | _CLONE | _PRUNE */
+  uint64_t seed;                  /* clone jitter: counter-based normals, deterministic */
+  gs_model_arrays adam_m_in, adam_v_in;   /* NULL members: not remapped */
+  void *workspace;
+  size_t workspace_bytes;
+  uint32_t *counters;             /* [4]: kept, split children per side, clones, n_out */
+  gs_model_arrays out, adam_m_out, adam_v_out;
+} gs_densify_args;
+size_t gs_densify_workspace_bytes(int32_t n);
+gs_status gs_densify_count(const gs_densify_args *a, gs_stream_t stream);
+gs_status gs_densify_emit(const gs_densify_args *a, gs_stream_t stream);
+
 /* ---- misc --------------------------------------------------------------- */
 int32_t gs_abi_version(void);
 const char *gs_last_error(void);

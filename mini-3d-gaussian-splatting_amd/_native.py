@@ -122,12 +122,32 @@ class GsLossArgs(C.Structure):
     ]
 
 
+GS_DENSIFY_SPLIT, GS_DENSIFY_CLONE, GS_DENSIFY_PRUNE = 1, 2, 4
+
+
+class GsModelArrays(C.Structure):
+    _fields_ = [("xyz", _vp), ("features_dc", _vp), ("features_rest", _vp), ("scaling", _vp),
+                ("rotation", _vp), ("opacity", _vp)]
+
+
+class GsDensifyArgs(C.Structure):
+    _fields_ = [
+        ("n", C.c_int32), ("rest_floats", C.c_int32), ("in_", GsModelArrays), ("xyz_grad", _vp),
+        ("grad_threshold", C.c_float), ("scene_extent", C.c_float), ("split_size", C.c_float),
+        ("clone_size", C.c_float), ("min_opacity", C.c_float), ("flags", C.c_int32), ("seed", C.c_uint64),
+        ("adam_m_in", GsModelArrays), ("adam_v_in", GsModelArrays), ("workspace", _vp),
+        ("workspace_bytes", C.c_size_t), ("counters", _vp), ("out", GsModelArrays),
+        ("adam_m_out", GsModelArrays), ("adam_v_out", GsModelArrays),
+    ]
+
+
 # Every symbol the header declares (checked by tests/test_abi.py).
 EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
     "gs_tile_ranges", "gs_blend_live_words", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
     "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
+    "gs_densify_workspace_bytes", "gs_densify_count", "gs_densify_emit",
 )
 
 _lib = None
@@ -162,9 +182,13 @@ def _declare(lib):
     lib.gs_loss_workspace_bytes.restype = C.c_size_t
     lib.gs_loss_forward.argtypes = [P(GsLossArgs), _vp]
     lib.gs_loss_backward.argtypes = [P(GsLossArgs), _vp]
+    lib.gs_densify_workspace_bytes.argtypes = [C.c_int32]
+    lib.gs_densify_workspace_bytes.restype = C.c_size_t
+    lib.gs_densify_count.argtypes = [P(GsDensifyArgs), _vp]
+    lib.gs_densify_emit.argtypes = [P(GsDensifyArgs), _vp]
     for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_bin_count", "gs_bin_emit",
               "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-              "gs_adam_step", "gs_loss_forward", "gs_loss_backward"):
+              "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
         getattr(lib, f).restype = C.c_int
 
 

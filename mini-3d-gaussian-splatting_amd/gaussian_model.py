@@ -1,10 +1,10 @@
 """GaussianModel with the reference's parameter layout and accessors
 (src/core/gaussian_model.py:15-128, 200-216).
 
-Only what the render path reads is here: parameters, activations,
-get_* accessors, covariance, random init.  Densification (reference
-:130-197) is a "next" row of SURVEY.md section 8(f) and is not part of this
-round's scope.
+Parameters, activations, get_* accessors, covariance, random init, and
+densification (reference :130-197) as one GPU
+compaction pass (gs_densify_count / gs_densify_emit) that also remaps the
+optimizer's Adam moments.
 
 Fixes relative to the reference, each a reference bug the render path trips
 over: get_covariance works (the reference calls a missing
@@ -15,9 +15,13 @@ from __future__ import annotations
 import math
 from typing import Optional
 
+import ctypes as C
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from . import _native as N
 
 
 def build_rotation_matrix(q: torch.Tensor) -> torch.Tensor:
@@ -145,3 +149,97 @@ class GaussianModel(nn.Module):
     def grad_parameters(self):
         """Parameters that receive a render gradient (features_rest does not)."""
         return [self._xyz, self._features_dc, self._scaling, self._rotation, self._opacity]
+
+    def parameter_list(self):
+        """The six parameters in gs_model_arrays order."""
+        return [self._xyz, self._features_dc, self._features_rest, self._scaling, self._rotation, self._opacity]
+
+    # -- densification (gaussian_model.py:130-197, optimizer.py:34-67) --------
+    @torch.no_grad()
+    def densify_and_prune(self, grad_threshold: float, scene_extent: float, min_opacity: float = 0.01,
+                          optimizer: Optional[torch.optim.Optimizer] = None, seed: Optional[int] = None,
+                          split: bool = True, clone: bool = True, prune: bool = True,
+                          xyz_grad: Optional[torch.Tensor] = None) -> dict:
+        """Split large / clone small high-gradient Gaussians, then drop those
+        with opacity <= min_opacity, in one GPU pass (semantics in
+        include/gsplat_mi355x.h, "Densification").  With `optimizer`, its
+        Adam moments follow the Gaussians (new ones start at zero) and its
+        parameter references are replaced.  Returns the output counts."""
+        params = self.parameter_list()
+        n, dev = self.get_num_points(), self._xyz.device
+        grad = xyz_grad if xyz_grad is not None else self._xyz.grad
+        for p in params:
+            if not (p.is_cuda and p.is_contiguous()):
+                raise RuntimeError("densify needs contiguous parameters on a HIP device")
+        if seed is None:
+            self._densify_calls = getattr(self, "_densify_calls", 0) + 1
+            seed = 0x5EED0000 + self._densify_calls
+        lib = N.load()
+        rest = int(self._features_rest[0].numel()) if n else 0
+        flags = (N.GS_DENSIFY_SPLIT if split else 0) | (N.GS_DENSIFY_CLONE if clone else 0) | \
+                (N.GS_DENSIFY_PRUNE if prune else 0)
+        states = [optimizer.state.get(p, {}) if optimizer is not None else {} for p in params]
+
+        def arrays(ts):
+            return N.GsModelArrays(*[N.ptr(t) for t in ts])
+
+        ws = torch.empty((max(int(lib.gs_densify_workspace_bytes(n)), 4),), dtype=torch.uint8, device=dev)
+        counters = torch.zeros((4,), dtype=torch.int32, device=dev)
+        g = None if grad is None else grad.detach().float().contiguous()
+        a = N.GsDensifyArgs()
+        a.n, a.rest_floats, a.in_ = n, rest, arrays(params)
+        a.xyz_grad = N.ptr(g)
+        a.grad_threshold, a.scene_extent = float(grad_threshold), float(scene_extent)
+        a.split_size, a.clone_size, a.min_opacity = 0.03, 0.01, float(min_opacity)
+        a.flags, a.seed = flags, int(seed) & 0xFFFFFFFFFFFFFFFF
+        a.adam_m_in = arrays([st.get("exp_avg") for st in states])
+        a.adam_v_in = arrays([st.get("exp_avg_sq") for st in states])
+        a.workspace, a.workspace_bytes, a.counters = N.ptr(ws), ws.numel(), N.ptr(counters)
+        stream = torch.cuda.current_stream().cuda_stream
+        N.check(lib.gs_densify_count(C.byref(a), stream), "gs_densify_count")
+        kept, nsplit, ncl, n_out = (int(v) for v in counters.tolist())
+        outs = [torch.empty((n_out,) + tuple(p.shape[1:]), dtype=p.dtype, device=dev) for p in params]
+        m_out = [torch.empty_like(o) if "exp_avg" in st else None for o, st in zip(outs, states)]
+        v_out = [torch.empty_like(o) if "exp_avg_sq" in st else None for o, st in zip(outs, states)]
+        a.out, a.adam_m_out, a.adam_v_out = arrays(outs), arrays(m_out), arrays(v_out)
+        N.check(lib.gs_densify_emit(C.byref(a), stream), "gs_densify_emit")
+        new = [nn.Parameter(o) for o in outs]
+        if optimizer is not None:
+            remap = {id(p): (q, st, m, v) for p, q, st, m, v in zip(params, new, states, m_out, v_out)}
+            for group in optimizer.param_groups:
+                group["params"] = [remap[id(p)][0] if id(p) in remap else p for p in group["params"]]
+            for p in params:
+                if p in optimizer.state:
+                    del optimizer.state[p]
+            for p, q, st, m, v in zip(params, new, states, m_out, v_out):
+                if st:
+                    nst = dict(st)
+                    if m is not None:
+                        nst["exp_avg"] = m
+                    if v is not None:
+                        nst["exp_avg_sq"] = v
+                    optimizer.state[q] = nst
+        (self._xyz, self._features_dc, self._features_rest, self._scaling, self._rotation,
+         self._opacity) = new
+        self.xyz_gradient_accum = torch.zeros(n_out, 3, device=dev)
+        self.denom = torch.zeros(n_out, 1, device=dev)
+        self.max_radii2D = torch.zeros(n_out, device=dev)
+        return {"kept": kept, "split": nsplit, "cloned": ncl, "n": n_out}
+
+    def density_and_split(self, grad_threshold: float, scene_extent: float) -> None:
+        """gaussian_model.py:131-157 (split only, no opacity prune)."""
+        self.densify_and_prune(grad_threshold, scene_extent, split=True, clone=False, prune=False)
+
+    def density_and_clone(self, grad_threshold: float, scene_extent: float) -> None:
+        """gaussian_model.py:160-178 (clone only, no opacity prune)."""
+        self.densify_and_prune(grad_threshold, scene_extent, split=False, clone=True, prune=False)
+
+    @torch.no_grad()
+    def prune_points(self, mask: torch.Tensor) -> None:
+        """gaussian_model.py:181-197: keep the Gaussians where mask is True."""
+        (self._xyz, self._features_dc, self._features_rest, self._scaling, self._rotation,
+         self._opacity) = [nn.Parameter(p.data[mask].contiguous()) for p in self.parameter_list()]
+        n, dev = self.get_num_points(), self._xyz.device
+        self.xyz_gradient_accum = torch.zeros(n, 3, device=dev)
+        self.denom = torch.zeros(n, 1, device=dev)
+        self.max_radii2D = torch.zeros(n, device=dev)
