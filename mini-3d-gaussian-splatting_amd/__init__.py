@@ -10,7 +10,12 @@ from .gaussian_model import GaussianModel, build_rotation_matrix  # noqa: F401
 from .camera import Camera, CameraUtils  # noqa: F401
 from .rasterizer import CameraParams, rasterize  # noqa: F401
 from .loss import SSIMLoss, GaussianLoss, photometric_loss  # noqa: F401
-from . import _native, synthetic, distributed, optim, loss  # noqa: F401
+from .config import TrainingConfig, ConfigManager  # noqa: F401
+from .dataset import CameraDataset, NeRFSyntheticDataset, COLMAPDataset, load_dataset  # noqa: F401
+from .trainer import GaussianTrainer  # noqa: F401
+from . import _native, synthetic, distributed, optim, loss, dataset, trainer  # noqa: F401
 
 __all__ = ["GaussianRenderer", "RenderSettings", "GaussianModel", "Camera", "CameraUtils",
-           "CameraParams", "rasterize", "camera_params", "SSIMLoss", "GaussianLoss", "photometric_loss"]
+           "CameraParams", "rasterize", "camera_params", "SSIMLoss", "GaussianLoss", "photometric_loss",
+           "TrainingConfig", "ConfigManager", "CameraDataset", "NeRFSyntheticDataset", "COLMAPDataset",
+           "load_dataset", "GaussianTrainer"]

@@ -55,3 +55,94 @@ class FusedAdam(torch.optim.Optimizer):
                     a.t[k] = d
                 N.check(lib.gs_adam_step(C.byref(a), stream), "gs_adam_step")
         return loss
+
+
+# --------------------------------------------------------------------------
+# Schedules and density control (reference src/core/optimizer.py:7-141)
+# --------------------------------------------------------------------------
+import math  # noqa: E402
+
+
+class LearningRateScheduler:
+    """optimizer.py:7-32: cosine from lr_init to lr_final over max_steps,
+    times the delay ramp lr_delay_mult -> 1 over lr_delay_steps."""
+
+    def __init__(self, lr_init: float, lr_final: float, lr_delay_steps: int, lr_delay_mult: float, max_steps: int):
+        self.lr_init, self.lr_final = lr_init, lr_final
+        self.lr_delay_steps, self.lr_delay_mult, self.max_steps = lr_delay_steps, lr_delay_mult, max_steps
+
+    def get_lr(self, step: int) -> float:
+        if self.max_steps <= 0:
+            return self.lr_final
+        t = min(step, self.max_steps) / self.max_steps
+        lr = self.lr_final + (self.lr_init - self.lr_final) * 0.5 * (1 + math.cos(math.pi * t))
+        if self.lr_delay_steps > 0:
+            lr *= self.lr_delay_mult + (1 - self.lr_delay_mult) * min(step / self.lr_delay_steps, 1)
+        return float(lr)
+
+
+class DensityController:
+    """optimizer.py:34-88: densify in [densify_from_iter, densify_until_iter]
+    every densify_interval iterations; split / clone by |dL/dxyz| and prune
+    opacity <= min_opacity in one GPU pass (GaussianModel.densify_and_prune),
+    the Adam state following the Gaussians."""
+
+    def __init__(self, config):
+        self.config = config
+
+    def should_densify(self, iteration: int) -> bool:
+        c = self.config
+        return c.densify_from_iter <= iteration <= c.densify_until_iter and iteration % c.densify_interval == 0
+
+    @torch.no_grad()
+    def densify_and_prune(self, gaussians, optimizer, iteration: int, scene_extent: float) -> dict:
+        return gaussians.densify_and_prune(self.config.densify_grad_threshold, scene_extent,
+                                           getattr(self.config, "min_opacity", 0.01), optimizer=optimizer,
+                                           seed=0x5EED0000 + iteration)
+
+
+class GaussianOptimizer:
+    """optimizer.py:90-141 with FusedAdam over the reference's five groups.
+    After densification the Adam moments are remapped (the reference's
+    setup_optimizer() would drop them, optimizer.py:133-137)."""
+
+    def __init__(self, gaussians, config):
+        self.gaussians, self.config = gaussians, config
+        self.optimizer = None
+        self.lr_scheduler = LearningRateScheduler(config.position_lr_init, config.position_lr_final, 0, 1.0,
+                                                  config.iterations)
+        self.density_controller = DensityController(config)
+
+    def setup_optimizer(self) -> None:
+        g, c = self.gaussians, self.config
+        self.optimizer = FusedAdam([
+            {"params": [g._xyz], "lr": c.position_lr_init},
+            {"params": [g._features_dc, g._features_rest], "lr": c.feature_lr},
+            {"params": [g._opacity], "lr": c.opacity_lr},
+            {"params": [g._scaling], "lr": c.scaling_lr},
+            {"params": [g._rotation], "lr": c.rotation_lr},
+        ])  # torch.optim.Adam defaults, as optimizer.py:109
+
+    def step(self) -> None:
+        self.optimizer.step()
+
+    def zero_grad(self) -> None:
+        self.optimizer.zero_grad(set_to_none=True)
+
+    def update_learning_rate(self, iteration: int) -> None:
+        """optimizer.py:120-129: every group follows the position schedule's ratio."""
+        base, c = self.lr_scheduler.get_lr(iteration), self.config
+        pg = self.optimizer.param_groups
+        pg[0]["lr"] = base
+        pg[1]["lr"] = base * (c.feature_lr / c.position_lr_init)
+        pg[2]["lr"] = base * (c.opacity_lr / c.position_lr_init)
+        pg[3]["lr"] = base * (c.scaling_lr / c.position_lr_init)
+        pg[4]["lr"] = base * (c.rotation_lr / c.position_lr_init)
+
+    def densify_and_prune(self, iteration: int, scene_extent: float):
+        if self.density_controller.should_densify(iteration):
+            return self.density_controller.densify_and_prune(self.gaussians, self.optimizer, iteration, scene_extent)
+        return None
+
+    def reset_opacity(self) -> None:
+        self.gaussians.reset_opacity()
