@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3
+#define GS_ABI_VERSION 4
 #define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_MAX_RECT_TILES 8   /* r <= 50 px -> an AABB spans at most 8 tiles per axis */
@@ -61,6 +61,7 @@ typedef struct gs_camera {
   float radius_max;      /* GaussianRenderer(radius_max=50.0) */
   float bg[3];           /* RenderSettings.bg_color */
   int32_t tile_size;     /* must be GS_TILE */
+  float campos[3];       /* camera centre in world coordinates, -R^T t; read only when sh_degree > 0 */
 } gs_camera;
 
 /* Gaussian inputs (the duck-typed GaussianModel accessors).
@@ -82,6 +83,17 @@ typedef struct gs_gaussians {
   int32_t opacity_is_logit;  /* 1: opacity holds the model's raw _opacity; the kernels apply
                                 get_opacity's sigmoid (gaussian_model.py:119-120) and d_opacity
                                 is the gradient w.r.t. the logit */
+  /* View-dependent colour (off by default).  The reference
+   * renders sigmoid(features[:,0,:]) only (renderer.py:88-92; its
+   * MathUtils.spherical_harmonics_eval returns coeffs[:,0], math_utils.py:45-49).
+   * sh_degree = 0 is exactly that.  sh_degree = d in 1..3 evaluates the
+   * degree-d real SH of the view direction dir = normalize(xyz - campos):
+   *   logit_c = color_logits[c] + sum_{k=1}^{(d+1)^2-1} Y_k(dir) sh_rest[k-1][c]
+   * (Y_k: the 3DGS basis constants and signs; the DC coefficient stays the
+   * raw logit, so degree 0 reduces to the reference), colour = sigmoid(logit). */
+  int32_t sh_degree;
+  const float *sh_rest;      /* [n, sh_rest_stride] rows holding [15,3] (get_features[:,1:,:]) */
+  int64_t sh_rest_stride;
 } gs_gaussians;
 
 /* ---- Stage 1: _project_gaussians_3d_to_2d + _frustum_culling ----------
@@ -215,7 +227,9 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
  * conics outputs, and chains through sigmoid(colour), inv(cov2d),
  * J cov_cam J^T, Rv Sigma Rv^T, the perspective Jacobian J(X,Y,Z) and
  * Xc = Rv Xw + Tv (autograd of renderer.py:117-200), and, on the raw path,
- * through Sigma(exp(s), normalize(q)) (gaussian_model.py:200-207). */
+ * through Sigma(exp(s), normalize(q)) (gaussian_model.py:200-207), and with
+ * sh_degree > 0 through the SH colour into sh_rest and (via the view
+ * direction) into xyz. */
 typedef struct gs_project_bwd_args {
   gs_camera cam;
   gs_gaussians g;
@@ -234,6 +248,7 @@ typedef struct gs_project_bwd_args {
   float *d_rotation;           /* [n,4]  (raw path)   */
   float *d_color_logits;       /* [n,3] */
   float *d_opacity;            /* [n]   */
+  float *d_sh_rest;            /* [n,15,3] contiguous, written when g.sh_degree > 0 (zeros past the degree) */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
 

@@ -24,7 +24,8 @@ GS_TILE = 16
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 3
+GS_ABI_VERSION = 4
+GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
 
@@ -34,7 +35,7 @@ class GsCamera(C.Structure):
         ("image_width", C.c_int32), ("image_height", C.c_int32),
         ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
         ("view", C.c_float * 12), ("radius_min", C.c_float), ("radius_max", C.c_float),
-        ("bg", C.c_float * 3), ("tile_size", C.c_int32),
+        ("bg", C.c_float * 3), ("tile_size", C.c_int32), ("campos", C.c_float * 3),
     ]
 
 
@@ -43,6 +44,7 @@ class GsGaussians(C.Structure):
         ("n", C.c_int32), ("xyz", _vp), ("xyz_stride", C.c_int64), ("cov3d", _vp),
         ("scaling", _vp), ("rotation", _vp), ("color_logits", _vp), ("color_stride", C.c_int64),
         ("opacity", _vp), ("opacity_stride", C.c_int64), ("opacity_is_logit", C.c_int32),
+        ("sh_degree", C.c_int32), ("sh_rest", _vp), ("sh_rest_stride", C.c_int64),
     ]
 
 
@@ -89,7 +91,7 @@ class GsProjectBwdArgs(C.Structure):
         ("cam", GsCamera), ("g", GsGaussians), ("means2d", _vp), ("conics", _vp), ("vis", _vp),
         ("rects", _vp), ("pair_offset", _vp), ("order", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
         ("g_conics", _vp), ("d_xyz", _vp), ("d_cov3d", _vp), ("d_scaling", _vp),
-        ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp),
+        ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
     ]
 
 

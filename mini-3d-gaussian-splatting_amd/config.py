@@ -44,6 +44,8 @@ class TrainingConfig:
     test_every: int = 8                # every k-th camera held out when a dataset has no test split
     log_interval: int = 100
     seed: int = 0
+    sh_degree: int = 0                 # max SH degree of the colour (0 = the reference's DC-only render)
+    sh_increase_interval: int = 1000   # active SH degree +1 every this many iterations, up to sh_degree
 
 
 class ConfigManager:

@@ -168,6 +168,89 @@ __device__ __forceinline__ void cov_from_raw(const float *sc, const float *rq, f
                      (R[i * 3 + 2] * s2[2]) * R[j * 3 + 2];
 }
 
+// ------------------------------------------------- view-dependent colour ----
+// Real SH basis Y_1..Y_15 (degrees 1..3) with the 3DGS constants and signs;
+// Y_0 is folded into the DC logit (gs_gaussians.sh_degree in the header).
+constexpr float kSH1 = 0.4886025119029199f;
+constexpr float kSH2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                           -1.0925484305920792f, 0.5462742152960396f};
+constexpr float kSH3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                           0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                           -0.5900435899266435f};
+
+__device__ __forceinline__ void sh_basis(float x, float y, float z, float Y[15]) {
+  const float xx = x * x, yy = y * y, zz = z * z;
+  Y[0] = -kSH1 * y;
+  Y[1] = kSH1 * z;
+  Y[2] = -kSH1 * x;
+  Y[3] = kSH2[0] * (x * y);
+  Y[4] = kSH2[1] * (y * z);
+  Y[5] = kSH2[2] * (2.f * zz - xx - yy);
+  Y[6] = kSH2[3] * (x * z);
+  Y[7] = kSH2[4] * (xx - yy);
+  Y[8] = kSH3[0] * y * (3.f * xx - yy);
+  Y[9] = kSH3[1] * (x * y) * z;
+  Y[10] = kSH3[2] * y * (4.f * zz - xx - yy);
+  Y[11] = kSH3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+  Y[12] = kSH3[4] * x * (4.f * zz - xx - yy);
+  Y[13] = kSH3[5] * z * (xx - yy);
+  Y[14] = kSH3[6] * x * (xx - 3.f * yy);
+}
+
+// dY_k/d(x, y, z) contracted with per-basis weights w[k] (the direction is
+// treated as free; the caller projects through the normalisation)
+__device__ __forceinline__ void sh_basis_vjp(float x, float y, float z, const float w[15], int nb, float d[3]) {
+  const float xx = x * x, yy = y * y, zz = z * z;
+  float dx = -kSH1 * w[2], dy = -kSH1 * w[0], dz = kSH1 * w[1];
+  if (nb > 3) {
+    dx += kSH2[0] * y * w[3] - 2.f * kSH2[2] * x * w[5] + kSH2[3] * z * w[6] + 2.f * kSH2[4] * x * w[7];
+    dy += kSH2[0] * x * w[3] + kSH2[1] * z * w[4] - 2.f * kSH2[2] * y * w[5] - 2.f * kSH2[4] * y * w[7];
+    dz += kSH2[1] * y * w[4] + 4.f * kSH2[2] * z * w[5] + kSH2[3] * x * w[6];
+  }
+  if (nb > 8) {
+    dx += 6.f * kSH3[0] * x * y * w[8] + kSH3[1] * y * z * w[9] - 2.f * kSH3[2] * x * y * w[10] -
+          6.f * kSH3[3] * x * z * w[11] + kSH3[4] * (4.f * zz - 3.f * xx - yy) * w[12] +
+          2.f * kSH3[5] * x * z * w[13] + kSH3[6] * (3.f * xx - 3.f * yy) * w[14];
+    dy += kSH3[0] * (3.f * xx - 3.f * yy) * w[8] + kSH3[1] * x * z * w[9] +
+          kSH3[2] * (4.f * zz - xx - 3.f * yy) * w[10] - 6.f * kSH3[3] * y * z * w[11] -
+          2.f * kSH3[4] * x * y * w[12] - 2.f * kSH3[5] * y * z * w[13] - 6.f * kSH3[6] * x * y * w[14];
+    dz += kSH3[1] * x * y * w[9] + 8.f * kSH3[2] * y * z * w[10] + kSH3[3] * (6.f * zz - 3.f * xx - 3.f * yy) * w[11] +
+          8.f * kSH3[4] * x * z * w[12] + kSH3[5] * (xx - yy) * w[13];
+  }
+  d[0] = dx;
+  d[1] = dy;
+  d[2] = dz;
+}
+
+__device__ __forceinline__ int sh_rest_count(int degree) { return (degree + 1) * (degree + 1) - 1; }
+
+// Colour logits of Gaussian g: the DC logits, plus the SH terms when enabled.
+// dir / inv_norm are returned for the backward.
+__device__ __forceinline__ void color_logits(const gs_gaussians &G, const gs_camera &c, int g, float xw, float yw,
+                                             float zw, float lg[3], float dir[3], float &inv_norm) {
+  const float *cl = G.color_logits + (int64_t)g * G.color_stride;
+  lg[0] = cl[0];
+  lg[1] = cl[1];
+  lg[2] = cl[2];
+  inv_norm = 0.f;
+  if (G.sh_degree <= 0) return;
+  const float vx = xw - c.campos[0], vy = yw - c.campos[1], vz = zw - c.campos[2];
+  const float nrm = sqrtf((vx * vx + vy * vy) + vz * vz);
+  inv_norm = 1.f / fmaxf(nrm, 1e-12f);
+  dir[0] = vx * inv_norm;
+  dir[1] = vy * inv_norm;
+  dir[2] = vz * inv_norm;
+  float Y[15];
+  sh_basis(dir[0], dir[1], dir[2], Y);
+  const int nb = sh_rest_count(G.sh_degree);
+  const float *r = G.sh_rest + (int64_t)g * G.sh_rest_stride;
+  for (int k = 0; k < nb; ++k) {
+    lg[0] += Y[k] * r[3 * k];
+    lg[1] += Y[k] * r[3 * k + 1];
+    lg[2] += Y[k] * r[3 * k + 2];
+  }
+}
+
 // =================================================== stage 1: projection ==
 __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
   const int g = blockIdx.x * kBlock + threadIdx.x;
@@ -254,7 +337,8 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
         ry = (uint32_t)(y0 / T) | ((uint32_t)((y1 - 1) / T) << 16);
         rinfo = (uint32_t)(x0 / T) | ((uint32_t)(y0 / T) << 12) | ((uint32_t)((x1 - 1) / T - x0 / T) << 24);
       }
-      const float *cl = a.g.color_logits + (int64_t)g * a.g.color_stride;
+      float cl[3], dir[3], inv_norm;
+      color_logits(a.g, c, g, xw, yw, zw, cl, dir, inv_norm);
       float op = a.g.opacity[(int64_t)g * a.g.opacity_stride];
       if (a.g.opacity_is_logit) op = 1.f / (1.f + expf(-op));  // get_opacity
       float4 *rec = reinterpret_cast<float4 *>(a.records) + 3 * (int64_t)g;
@@ -992,12 +1076,38 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) G[k] += a.g_conics[4 * (size_t)g + k];
   }
-  // colour: sigmoid chain (renderer.py:90)
-  const float *cl = a.g.color_logits + (int64_t)g * a.g.color_stride;
+  // colour: sigmoid chain (renderer.py:90), and the SH terms when enabled
+  const float *X3 = a.g.xyz + (int64_t)g * a.g.xyz_stride;
+  float cl[3], dir[3], inv_norm;
+  color_logits(a.g, a.cam, g, X3[0], X3[1], X3[2], cl, dir, inv_norm);
+  float dlg[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float c = 1.f / (1.f + expf(-cl[k]));
-    a.d_color_logits[3 * (size_t)g + k] = acc[6 + k] * c * (1.f - c);
+    dlg[k] = acc[6 + k] * c * (1.f - c);
+    a.d_color_logits[3 * (size_t)g + k] = dlg[k];
+  }
+  // SH: d rest_k = Y_k dlogit; the view direction's gradient reaches xyz
+  // through dir = v / |v| (added to d_xyz below)
+  double dxyz_sh[3] = {0.0, 0.0, 0.0};
+  if (a.g.sh_degree > 0) {
+    const int nb = sh_rest_count(a.g.sh_degree);
+    const float *r = a.g.sh_rest + (int64_t)g * a.g.sh_rest_stride;
+    float Y[15], wY[15];
+    sh_basis(dir[0], dir[1], dir[2], Y);
+    float *dr = a.d_sh_rest + (size_t)g * 3 * 15;
+    for (int k = 0; k < 15; ++k) {
+      const bool on = k < nb;
+      dr[3 * k] = on ? Y[k] * dlg[0] : 0.f;
+      dr[3 * k + 1] = on ? Y[k] * dlg[1] : 0.f;
+      dr[3 * k + 2] = on ? Y[k] * dlg[2] : 0.f;
+      wY[k] = on ? (r[3 * k] * dlg[0] + r[3 * k + 1] * dlg[1]) + r[3 * k + 2] * dlg[2] : 0.f;
+    }
+    float dd[3];
+    sh_basis_vjp(dir[0], dir[1], dir[2], wY, nb, dd);
+    const double dot = (double)dir[0] * dd[0] + (double)dir[1] * dd[1] + (double)dir[2] * dd[2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dxyz_sh[j] = (dd[j] - dir[j] * dot) * inv_norm;
   }
   float dop = acc[5];
   if (a.g.opacity_is_logit) {  // through get_opacity's sigmoid, as torch's sigmoid_backward
@@ -1010,7 +1120,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   const bool raw = a.g.cov3d == nullptr;
   if (!any) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.d_xyz[3 * (size_t)g + k] = 0.f;
+    for (int k = 0; k < 3; ++k) a.d_xyz[3 * (size_t)g + k] = (float)dxyz_sh[k];
     if (raw) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) a.d_scaling[3 * (size_t)g + k] = 0.f;
@@ -1024,7 +1134,6 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   }
   const gs_camera &c = a.cam;
   const float *R = c.view;
-  const float *X3 = a.g.xyz + (int64_t)g * a.g.xyz_stride;
   float Sf[9];
   if (!raw) {
 #pragma unroll
@@ -1104,7 +1213,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
                     (double)acc[9];
 #pragma unroll
   for (int j = 0; j < 3; ++j)
-    a.d_xyz[3 * (size_t)g + j] = (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ);
+    a.d_xyz[3 * (size_t)g + j] = (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ + dxyz_sh[j]);
   if (!raw) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) a.d_cov3d[9 * (size_t)g + k] = (float)dS[k];
@@ -1228,6 +1337,8 @@ gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream) {
     return fail(GS_ERR_INVALID_ARG, "%s: null pointer", "gs_project_forward");
   if (!a->g.cov3d && (!a->g.scaling || !a->g.rotation))
     return fail(GS_ERR_INVALID_ARG, "%s: need cov3d or scaling+rotation", "gs_project_forward");
+  if (a->g.sh_degree < 0 || a->g.sh_degree > 3 || (a->g.sh_degree > 0 && !a->g.sh_rest))
+    return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest when > 0", "gs_project_forward");
   k_project_fwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_forward");
 }
@@ -1351,6 +1462,9 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
       !a->pair_offset || !a->d_xyz || !a->d_color_logits || !a->d_opacity ||
       (raw ? (!a->g.scaling || !a->g.rotation || !a->d_scaling || !a->d_rotation) : !a->d_cov3d))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_project_backward");
+  if (a->g.sh_degree < 0 || a->g.sh_degree > 3 || (a->g.sh_degree > 0 && (!a->g.sh_rest || !a->d_sh_rest)))
+    return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest and d_sh_rest when > 0",
+                "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
   k_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_backward");

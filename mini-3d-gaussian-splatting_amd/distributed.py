@@ -7,7 +7,8 @@ torch.distributed (backend "nccl" = RCCL over xGMI on MI355X, "gloo" on CPU
 for tests), issued after the last backward kernel and before
 optimizer.step().  Payload: xyz 3 + features_dc 3 + scaling 3 + rotation 4 +
 opacity 1 = 14 fp32 (56 B) per Gaussian; features_rest has an identically
-zero render gradient and is not sent.
+zero render gradient and is not sent unless SH colour is on
+(GaussianModel.grad_parameters: +45 fp32 per Gaussian then).
 """
 from __future__ import annotations
 

@@ -45,6 +45,9 @@ class GaussianModel(nn.Module):
         super().__init__()
         self.config = config
         self.max_sh_degree = max_sh_degree
+        # SH degree the renderer evaluates (RenderSettings.sh_degree=None reads
+        # it).  0 = the reference's DC-only colour; raised by oneup_sh_degree().
+        self.active_sh_degree = 0
         self._xyz = nn.Parameter(torch.empty(0, 3))
         self._features_dc = nn.Parameter(torch.empty(0, 1, 3))
         self._features_rest = nn.Parameter(torch.empty(0, 15, 3))
@@ -58,6 +61,11 @@ class GaussianModel(nn.Module):
         self.scaling_inverse_activation = torch.log
         self.opacity_activation = torch.sigmoid
         self.rotation_activation = F.normalize
+
+    def oneup_sh_degree(self) -> None:
+        """Raise the rendered SH degree by one, up to max_sh_degree."""
+        if self.active_sh_degree < self.max_sh_degree:
+            self.active_sh_degree += 1
 
     # -- init -------------------------------------------------------------
     def _set(self, xyz, fdc, frest, scaling, rot, opacity):
@@ -147,8 +155,12 @@ class GaussianModel(nn.Module):
         return torch.log(x / (1 - x))
 
     def grad_parameters(self):
-        """Parameters that receive a render gradient (features_rest does not)."""
-        return [self._xyz, self._features_dc, self._scaling, self._rotation, self._opacity]
+        """Parameters that receive a render gradient (features_rest only while
+        SH colour is on, active_sh_degree > 0)."""
+        ps = [self._xyz, self._features_dc, self._scaling, self._rotation, self._opacity]
+        if self.active_sh_degree > 0:
+            ps.insert(2, self._features_rest)
+        return ps
 
     def parameter_list(self):
         """The six parameters in gs_model_arrays order."""

@@ -56,7 +56,17 @@ class CameraParams:
         c.radius_min, c.radius_max = self.radius_min, self.radius_max
         c.bg = (C.c_float * 3)(*self.bg)
         c.tile_size = N.GS_TILE
+        c.campos = (C.c_float * 3)(*self.campos)
         return c
+
+    @property
+    def campos(self) -> Tuple[float, float, float]:
+        """Camera centre in world coordinates, -R^T t of the W2C view (the SH
+        view direction's origin)."""
+        v = self.view
+        R = ((v[0], v[1], v[2]), (v[4], v[5], v[6]), (v[8], v[9], v[10]))
+        t = (v[3], v[7], v[11])
+        return tuple(-(R[0][j] * t[0] + R[1][j] * t[1] + R[2][j] * t[2]) for j in range(3))
 
 
 def _rows(t: torch.Tensor, cols: int) -> Tuple[torch.Tensor, int]:
@@ -68,7 +78,8 @@ def _rows(t: torch.Tensor, cols: int) -> Tuple[torch.Tensor, int]:
     return t, t.stride(0)
 
 
-def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False) -> N.GsGaussians:
+def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
+                      sh_rest=None, sh_degree=0) -> N.GsGaussians:
     g = N.GsGaussians()
     g.n = n
     g.xyz, g.xyz_stride = N.ptr(xyz), xyz.stride(0)
@@ -77,6 +88,8 @@ def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity
     g.color_logits, g.color_stride = N.ptr(logits), logits.stride(0)
     g.opacity, g.opacity_stride = N.ptr(opacity), opacity.stride(0)
     g.opacity_is_logit = 1 if opacity_is_logit else 0
+    if sh_degree > 0:
+        g.sh_degree, g.sh_rest, g.sh_rest_stride = int(sh_degree), N.ptr(sh_rest), sh_rest.stride(0)
     return g
 
 
@@ -141,7 +154,8 @@ def _alloc_tile_buffers(lib, cap: int, num_tiles: int, dev):
     return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
 
 
-def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False):
+def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
+                     sh_rest=None, sh_degree=0):
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -149,7 +163,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     f32, i32 = torch.float32, torch.int32
     s = _stream()
     cs = cam.to_struct()
-    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit)
+    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
 
     means2d = torch.empty((n, 2), dtype=f32, device=dev)
     conics = torch.empty((n, 2, 2), dtype=f32, device=dev)
@@ -255,7 +269,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
 
 
 def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotation, logits, opacity,
-                      means2d, conics, g_image, g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit=False):
+                      means2d, conics, g_image, g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit=False,
+                      sh_rest=None, sh_degree=0):
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -286,16 +301,17 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     d_op = torch.empty((n,), dtype=f32, device=dev)
     gm = None if g_means2d is None else g_means2d.contiguous()
     gc = None if g_conics is None else g_conics.contiguous()
-    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit)
+    d_sh = torch.empty((n, N.GS_SH_REST, 3), dtype=f32, device=dev) if sh_degree > 0 else None
+    gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
     pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
                             # Gaussian order (order=NULL): inputs/outputs stream; walking in depth
                             # order coalesces the slot reads but scatters 10 arrays (measured 2.4x slower)
                             N.ptr(fr.pair_offset), None, N.ptr(pair_grads), N.ptr(gm), N.ptr(gc), N.ptr(d_xyz),
-                            N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op))
+                            N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op), N.ptr(d_sh))
     StageTimer.mark("project_bwd")
     N.check(lib.gs_project_backward(C.byref(pb), s), "gs_project_backward")
     StageTimer.mark("~end_bwd")
-    return d_xyz, d_cov, d_scl, d_rot, d_col, d_op
+    return d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh
 
 
 class RasterizeGaussians(torch.autograd.Function):
@@ -303,22 +319,24 @@ class RasterizeGaussians(torch.autograd.Function):
     are (image, alpha, depth, viewspace_points, conics, radii, visibility)."""
 
     @staticmethod
-    def forward(ctx, xyz, cov3d, scaling, rotation, logits, opacity, cam: CameraParams, opacity_is_logit=False):
+    def forward(ctx, xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, cam: CameraParams,
+                opacity_is_logit=False, sh_degree=0):
         image, alpha, depth, means2d, conics, radii, vis, fr = forward_pipeline(
-            cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit)
-        ctx.cam, ctx.frame, ctx.opacity_is_logit = cam, fr, opacity_is_logit
-        ctx.save_for_backward(xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics)
+            cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
+        ctx.cam, ctx.frame, ctx.opacity_is_logit, ctx.sh_degree = cam, fr, opacity_is_logit, sh_degree
+        ctx.save_for_backward(xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics)
         ctx.mark_non_differentiable(radii, vis)
         ctx.set_materialize_grads(False)
         return image, alpha, depth, means2d, conics, radii, vis
 
     @staticmethod
     def backward(ctx, g_image, g_alpha, g_depth, g_means2d, g_conics, _g_radii, _g_vis):
-        xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics = ctx.saved_tensors
+        xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics = ctx.saved_tensors
         g_conics = None if g_conics is None else g_conics.reshape(-1, 4)
-        d_xyz, d_cov, d_scl, d_rot, d_col, d_op = backward_pipeline(
+        d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh = backward_pipeline(
             ctx.cam, ctx.frame, xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics,
-            g_image, None if g_alpha is None else g_alpha, g_depth, g_means2d, g_conics, ctx.opacity_is_logit)
+            g_image, None if g_alpha is None else g_alpha, g_depth, g_means2d, g_conics, ctx.opacity_is_logit,
+            sh_rest, ctx.sh_degree)
         need = ctx.needs_input_grad
         return (d_xyz if need[0] else None,
                 d_cov if (cov3d is not None and need[1]) else None,
@@ -326,13 +344,28 @@ class RasterizeGaussians(torch.autograd.Function):
                 d_rot if (rotation is not None and need[3]) else None,
                 d_col if need[4] else None,
                 d_op.view(opacity.shape) if need[5] else None,
-                None, None)
+                d_sh if (sh_rest is not None and need[6]) else None,
+                None, None, None)
 
 
-def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False):
+def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
+              sh_rest=None, sh_degree=0):
     """opacity_is_logit: opacity holds the model's raw _opacity and the kernels
-    apply get_opacity's sigmoid (fused; its gradient goes to the logit)."""
+    apply get_opacity's sigmoid (fused; its gradient goes to the logit).
+    sh_degree > 0: view-dependent colour from sh_rest ([N,15,3] rest
+    coefficients, e.g. get_features[:,1:,:]); 0 is the reference's DC-only
+    colour (include/gsplat_mi355x.h, gs_gaussians)."""
     _check_inputs(xyz)
+    sh_degree = int(sh_degree)
+    if not 0 <= sh_degree <= 3:
+        raise ValueError(f"sh_degree must be in 0..3, got {sh_degree}")
+    if sh_degree > 0:
+        if sh_rest is None or tuple(sh_rest.shape[1:]) != (N.GS_SH_REST, 3):
+            raise ValueError("sh_degree > 0 needs sh_rest of shape [N, 15, 3]")
+        if sh_rest.stride(2) != 1 or sh_rest.stride(1) != 3:
+            sh_rest = sh_rest.contiguous()
+    else:
+        sh_rest = None
     if cov3d is not None:
         cov3d = cov3d.reshape(-1, 3, 3)
         if not cov3d.is_contiguous():
@@ -343,4 +376,5 @@ def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity,
     xyz, _ = _rows(xyz, 3)
     logits, _ = _rows(logits, 3)
     opacity, _ = _rows(opacity, 1)
-    return RasterizeGaussians.apply(xyz, cov3d, scaling, rotation, logits, opacity, cam, bool(opacity_is_logit))
+    return RasterizeGaussians.apply(xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, cam,
+                                    bool(opacity_is_logit), sh_degree)

@@ -21,12 +21,16 @@ Differences a caller can observe (all documented in DESIGN.md):
   * `radii` and `visibility_filter` carry no gradient.
   * `settings.scale_modifier` and `settings.debug` are ignored, as in the
     reference.
+  * `settings.sh_degree` (default: the model's `active_sh_degree`, else 0)
+    switches on view-dependent SH colour; at 0 -- the default for the
+    reference's own model and stubs -- colours are the reference's
+    sigmoid(DC).
 """
 from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 
@@ -41,6 +45,11 @@ class RenderSettings:
     bg_color: torch.Tensor
     scale_modifier: float = 1.0
     debug: bool = False
+    # View-dependent colour (not in the reference, which renders
+    # DC only): None takes `gaussians.active_sh_degree` when the model has one,
+    # else 0 (the reference's behaviour).  1..3 evaluates SH of that degree from
+    # get_features[:, 1:, :] (include/gsplat_mi355x.h, gs_gaussians).
+    sh_degree: Optional[int] = None
 
 
 def _world_view(camera) -> torch.Tensor:
@@ -87,14 +96,21 @@ class GaussianRenderer:
             logits = gaussians._features_dc.squeeze(1)
         else:
             cov3d, scaling, rotation = gaussians.get_covariance, None, None
-            feats = gaussians.get_features
+            feats = gaussians.get_features  # one read: the SH rest below is a view of it
             if feats.dim() == 3 and feats.shape[1] >= 1:
                 logits = feats[:, 0, :]
             else:
                 logits = gaussians._features_dc.squeeze(1)
         opacity = gaussians._opacity.squeeze(1) if fused else gaussians.get_opacity.squeeze(1)
+        sh_degree = settings.sh_degree
+        if sh_degree is None:
+            sh_degree = int(getattr(gaussians, "active_sh_degree", 0))
+        sh_rest = None
+        if sh_degree > 0:
+            sh_rest = gaussians._features_rest if fused else feats[:, 1:, :]
         image, alpha, depth, means2d, conics, radii, vis = rasterize(
-            cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=fused)
+            cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=fused,
+            sh_rest=sh_rest, sh_degree=sh_degree)
         return {
             "image": image,
             "alpha": alpha,

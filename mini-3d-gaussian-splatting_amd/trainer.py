@@ -86,6 +86,11 @@ class GaussianTrainer:
     # -- one step (trainer.py:65-69) ---------------------------------------
     def train_step(self, camera) -> Dict[str, torch.Tensor]:
         g, opt = self.gaussians, self.optimizer
+        c = self.config
+        if (c.sh_degree > g.active_sh_degree and c.sh_increase_interval > 0
+                and self.iteration > 0 and self.iteration % c.sh_increase_interval == 0):
+            g.max_sh_degree = max(g.max_sh_degree, c.sh_degree)
+            g.oneup_sh_degree()
         opt.zero_grad()
         out = self.renderer.render(camera, g, self._settings(camera))
         target = camera._image
@@ -148,7 +153,8 @@ class GaussianTrainer:
                 tensors[f"adam.{name}.v"] = st["exp_avg_sq"].contiguous()
                 tensors[f"adam.{name}.step"] = torch.tensor([st["step"]], dtype=torch.int64)
         path = self._ckpt_path(iteration)
-        save_file({k: v.cpu() for k, v in tensors.items()}, path, metadata={"iteration": str(iteration)})
+        save_file({k: v.cpu() for k, v in tensors.items()}, path,
+                  metadata={"iteration": str(iteration), "active_sh_degree": str(self.gaussians.active_sh_degree)})
         return path
 
     def load_checkpoint(self, iteration: int) -> None:
@@ -170,6 +176,7 @@ class GaussianTrainer:
                                                      "exp_avg": t[f"adam.{name}.m"].to(dev),
                                                      "exp_avg_sq": t[f"adam.{name}.v"].to(dev)}
         self.iteration = int(meta.get("iteration", iteration))
+        self.gaussians.active_sh_degree = int(meta.get("active_sh_degree", 0))
 
 
 __all__ = ["GaussianTrainer", "TrainingConfig"]

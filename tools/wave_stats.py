@@ -56,7 +56,8 @@ def main():
     L = 23.1 * 1.001
     tot = {k: torch.zeros((), dtype=torch.long, device=dev)
            for k in ("processed", "live", "bbox", "live_notbbox", "bwd_lockstep", "bwd_max", "bwd_sum",
-                     "bwd_entries", "bwd_entries_live", "bwd_live_max", "bwd_live_sum")}
+                     "bwd_entries", "bwd_entries_live", "bwd_live_max", "bwd_live_sum",
+                     "h_processed", "h_live", "v_processed", "v_live", "lanes_live", "h_bwd_max", "h_bwd_sum")}
     ys, xs = torch.meshgrid(torch.arange(8, device=dev), torch.arange(8, device=dev), indexing="ij")
     ys, xs = ys.reshape(-1).float(), xs.reshape(-1).float()
     num_tiles = tx_n * ty_n
@@ -86,6 +87,25 @@ def main():
             x0, y0 = tx * 16 + qx, ty * 16 + qy
             bb = ((mx + hx >= x0[None]) & (mx - hx <= x0[None] + 7) &
                   (my + hy >= y0[None]) & (my - hy <= y0[None] + 7))
+            # halves: rows (top/bottom 16x8: quadrants {0,1},{2,3}) and
+            # columns (left/right 8x16: {0,2},{1,3}); a half processes an entry
+            # up to its deepest lane, and is live if some lane of it is
+            lvq = (sq <= 23.1)                                                  # [n,4,64]
+            for key, pairs in (("h", ((0, 1), (2, 3))), ("v", ((0, 2), (1, 3)))):
+                for a_, b_ in pairs:
+                    ph = torch.arange(n, device=dev) < torch.maximum(qmax[t][a_], qmax[t][b_])
+                    tot[key + "_processed"] += ph.sum()
+                    tot[key + "_live"] += (ph & (lvq[:, a_].any(1) | lvq[:, b_].any(1))).sum()
+            tot["lanes_live"] += (lvq & proc[:, :, None]).sum()
+            hstop = int(qmax[t].max())
+            if hstop > 0:
+                hl = torch.stack([live[:hstop, 0] | live[:hstop, 1], live[:hstop, 2] | live[:hstop, 3]], 1).float()
+                nbh = (hstop + 15) // 16
+                hp = torch.zeros(nbh * 16, 2, device=dev)
+                hp[:hstop] = hl
+                perh = hp.view(nbh, 16, 2).sum(1)
+                tot["h_bwd_max"] += (2 * perh.max(1).values).sum().long()
+                tot["h_bwd_sum"] += perh.sum().long()
             tot["processed"] += proc.sum()
             tot["live"] += live.sum()
             tot["bbox"] += (proc & bb).sum()
@@ -125,6 +145,11 @@ def main():
     print(f"backward entries up to the tile stop {tot['bwd_entries']}, with a live quadrant {tot['bwd_entries_live']}; "
           f"compacted batches: busiest-wave {tot['bwd_live_max']}, decoupled {tot['bwd_live_sum']}")
     p = tot["processed"]
+    print(f"halves: rows live/processed {tot['h_live']}/{tot['h_processed']}, cols {tot['v_live']}/{tot['v_processed']}; "
+          f"quadrant live wave-entries {tot['live']} -> half (rows) {tot['h_live']} "
+          f"(x2 pixels/lane: {2 * tot['h_live'] / max(1, tot['live']):.3f} of the quadrant cost per entry-pixel-lane); "
+          f"lane efficiency in live quadrant wave-entries {tot['lanes_live'] / max(1, 64 * tot['live']):.3f}; "
+          f"bwd phase-A halves busiest-wave {tot['h_bwd_max']} decoupled {tot['h_bwd_sum']}")
     print(f"live/processed = {tot['live'] / p:.3f}, bbox/processed = {tot['bbox'] / p:.3f}, "
           f"evaluated pairs (E) = {int(neval.sum())}, processed lane-pairs = {64 * p}")
 
