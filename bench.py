@@ -121,7 +121,8 @@ def main():
     renderer = pkg.GaussianRenderer()
     g = torch.Generator().manual_seed(1)
     cot = [(torch.rand(s, generator=g) * 2 - 1).to(dev) for s in ((3, H, W), (1, H, W), (1, H, W))]
-    reducer = pkg.distributed.GradAllReduce(params, dist) if dist is not None else None
+    # the backward writes the gradients straight into the all-reduce bucket
+    reducer = pkg.distributed.GradAllReduce(params, dist).attach(model) if dist is not None else None
     frames = []
 
     # Every step renders the same scene: the parameters are restored from this

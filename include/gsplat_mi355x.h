@@ -31,11 +31,11 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4
+#define GS_ABI_VERSION 5
 #define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_MAX_RECT_TILES 8   /* r <= 50 px -> an AABB spans at most 8 tiles per axis */
-#define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian) gradient slot */
+#define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian, 8x8 quadrant) gradient partial */
 #define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2..3] reserved */
 
 typedef enum gs_status {
@@ -134,10 +134,13 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
  * gs_bin_count: per-Gaussian tile-touch counts and visibility in depth order,
  *   reduced to per-block partial sums and scanned; the callee zeroes
  *   counters, then counters[0] = M (visible), counters[1] = T (touches).
+ *   It also numbers the gradient slots (one per touched tile) in
+ *   Gaussian-index order, a Gaussian's slots consecutive: pair_offset is
+ *   written here (chunk-local) and completed by gs_bin_emit.
  * gs_bin_emit : one (tile id, Gaussian id) entry per touched tile, emitted in
  *   depth order (so a stable sort by tile keeps depth order inside a tile),
- *   written coalesced; pair_offset[g] = first entry of g, also stored in the
- *   Gaussian's record (word 7) for the backward's slot addressing. */
+ *   written coalesced; pair_offset[g] = g's first gradient slot, also stored
+ *   in the Gaussian's record (word 10) for the backward's slot addressing. */
 size_t gs_bin_workspace_bytes(int32_t n);
 typedef struct gs_bin_args {
   int32_t n;
@@ -148,11 +151,11 @@ typedef struct gs_bin_args {
   uint32_t *counters;         /* [GS_NUM_COUNTERS] */
   void *workspace;
   size_t workspace_bytes;
-  /* emit outputs (ignored by gs_bin_count) */
+  /* emit outputs (tile_keys / pair_gauss / records ignored by gs_bin_count) */
   uint32_t *tile_keys;   /* [T] */
   uint32_t *pair_gauss;  /* [T] */
-  uint32_t *pair_offset; /* [n] indexed by Gaussian id */
-  float *records;        /* [n, GS_RECORD_FLOATS]: word 7 <- pair_offset bits */
+  uint32_t *pair_offset; /* [n] indexed by Gaussian id: first gradient slot (both calls write it) */
+  float *records;        /* [n, GS_RECORD_FLOATS]: word 10 <- pair_offset bits */
 } gs_bin_args;
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream);
 gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream);
@@ -199,11 +202,15 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
 size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles);
 
 /* ---- Backward of the blend -------------------------------------------
- * Re-walks each pixel's list front-to-back (bit-identical replay of the
- * forward's decisions) and writes one gradient slot per (tile, Gaussian)
- * entry: pair_grads[e] = {dmu_x, dmu_y, dQ00, dQ01(=dQ10), dQ11, d_opacity,
- * d_r, d_g, d_b, d_z}, e = the entry's emit index (pair_offset[g] + its
- * tile's index in g's rectangle).  No atomics: deterministic. */
+ * One 64-lane workgroup per (tile, 8x8 quadrant), independent of the
+ * others: re-walks each pixel's list front-to-back (bit-identical replay of
+ * the forward's decisions) over the entries the forward's liveness bitmap
+ * marks for the quadrant, and writes one partial gradient per (entry,
+ * quadrant): pair_grads[4e + q] = {dmu_x, dmu_y, dQ00, dQ01(=dQ10), dQ11,
+ * d_opacity, d_r, d_g, d_b, d_z} over quadrant q's pixels, and sets
+ * slot_live[4e + q] = 1; e = the entry's gradient slot (pair_offset[g] + its
+ * tile's index in g's rectangle).  Partials of quadrants that did not replay
+ * the entry are not written.  No atomics: deterministic. */
 typedef struct gs_blend_bwd_args {
   gs_camera cam;
   int32_t tiles_x, tiles_y;
@@ -217,13 +224,14 @@ typedef struct gs_blend_bwd_args {
   const float *g_depth;         /* [H,W] or NULL */
   const uint64_t *live_bits;    /* the forward's liveness bitmap */
   int64_t live_words;
-  float *pair_grads;            /* [T, GS_PAIR_GRAD_FLOATS] */
+  float *pair_grads;            /* [T, 4, GS_PAIR_GRAD_FLOATS] */
+  uint8_t *slot_live;           /* [T, 4], zeroed by the caller */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
 
 /* ---- Backward of the projection ----------------------------------------
- * Sums each Gaussian's pair slots (contiguous: [pair_offset[g],
- * pair_offset[g] + touches)), adds cotangents on the viewspace_points /
+ * Sums each Gaussian's slot partials (slots [pair_offset[g], pair_offset[g]
+ * + touches), the quadrants slot_live flags), adds cotangents on the viewspace_points /
  * conics outputs, and chains through sigmoid(colour), inv(cov2d),
  * J cov_cam J^T, Rv Sigma Rv^T, the perspective Jacobian J(X,Y,Z) and
  * Xc = Rv Xw + Tv (autograd of renderer.py:117-200), and, on the raw path,
@@ -237,9 +245,9 @@ typedef struct gs_project_bwd_args {
   const uint8_t *vis;
   const uint32_t *rects;
   const uint32_t *pair_offset;
-  const uint32_t *order;       /* [n] permutation to walk the Gaussians in (the depth-sorted
-                                  ids: their slot ranges are then adjacent, reads coalesce); or NULL */
-  const float *pair_grads;     /* may be NULL when T == 0 */
+  const uint32_t *order;       /* [n] permutation to walk the Gaussians in, or NULL: index order
+                                  (slots are numbered in index order, so NULL reads them coalesced) */
+  const float *pair_grads;     /* [T,4,GS_PAIR_GRAD_FLOATS]; may be NULL when T == 0 */
   const float *g_means2d;      /* [n,2] or NULL */
   const float *g_conics;       /* [n,4] or NULL */
   float *d_xyz;                /* [n,3] */
@@ -249,6 +257,9 @@ typedef struct gs_project_bwd_args {
   float *d_color_logits;       /* [n,3] */
   float *d_opacity;            /* [n]   */
   float *d_sh_rest;            /* [n,15,3] contiguous, written when g.sh_degree > 0 (zeros past the degree) */
+  const uint8_t *slot_live;    /* [T,4] from gs_blend_backward; required with pair_grads */
+  float *slot_sums;            /* [T, GS_PAIR_GRAD_FLOATS] scratch (quadrant partials summed); with pair_grads */
+  int64_t num_slots;           /* T */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
 

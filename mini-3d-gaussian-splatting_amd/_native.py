@@ -24,7 +24,7 @@ GS_TILE = 16
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 4
+GS_ABI_VERSION = 5
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -82,7 +82,7 @@ class GsBlendBwdArgs(C.Structure):
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
         ("sorted_gauss", _vp), ("records", _vp), ("pix_acc", _vp),
         ("pix_state", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp),
-        ("live_bits", _vp), ("live_words", C.c_int64), ("pair_grads", _vp),
+        ("live_bits", _vp), ("live_words", C.c_int64), ("pair_grads", _vp), ("slot_live", _vp),
     ]
 
 
@@ -92,6 +92,8 @@ class GsProjectBwdArgs(C.Structure):
         ("rects", _vp), ("pair_offset", _vp), ("order", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
         ("g_conics", _vp), ("d_xyz", _vp), ("d_cov3d", _vp), ("d_scaling", _vp),
         ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
+        ("slot_live", _vp), ("slot_sums", _vp),
+        ("num_slots", C.c_int64),
     ]
 
 

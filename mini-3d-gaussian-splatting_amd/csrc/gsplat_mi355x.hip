@@ -17,6 +17,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "gsplat_mi355x.h"
 #include "gs_internal.h"
 
@@ -77,6 +79,17 @@ __device__ __forceinline__ float exp_inrange(float x) {
   const float ph = x * 0x1.715476p+0f;
   float pl = __builtin_fmaf(x, 0x1.715476p+0f, -ph);
   pl = __builtin_fmaf(x, 0x1.4ae0bep-26f, pl);
+  const float r = __builtin_amdgcn_exp2f(ph);
+  return __builtin_fmaf(r, pl * 0x1.62e430p-1f, r);
+}
+
+// exp(-s/2) for s in [0, 23.1]: exp_inrange(-0.5f * s) with the -1/2 folded
+// into the constants -- scaling by a power of two is exact, so every product
+// (and each fma's exact product) is the same real number: bit-identical.
+__device__ __forceinline__ float exp_neg_half(float s) {
+  const float ph = s * -0x1.715476p-1f;
+  float pl = __builtin_fmaf(s, -0x1.715476p-1f, -ph);
+  pl = __builtin_fmaf(s, -0x1.4ae0bep-27f, pl);
   const float r = __builtin_amdgcn_exp2f(ph);
   return __builtin_fmaf(r, pl * 0x1.62e430p-1f, r);
 }
@@ -491,6 +504,25 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
     partials[blockIdx.x] = tot;
     partials[nb + blockIdx.x] = totv;
   }
+  // Gradient slots are numbered in Gaussian-index order (a Gaussian's
+  // touches consecutive), so that gs_project_backward's threads g, g+1 read
+  // adjacent slot ranges: here each Gaussian's exclusive prefix of touches
+  // inside this block's index chunk (k_bin_emit adds the chunk's offset).
+  uint32_t carry = 0;
+  for (int i = 0; i < kBinChunk / kBlock; ++i) {
+    const long long g = base + i * kBlock + threadIdx.x;
+    uint32_t cnt = 0;
+    if (g < a.n) {
+      int tx0, tx1, ty0, ty1;
+      unpack_rect(a.rects, (uint32_t)g, tx0, tx1, ty0, ty1);
+      cnt = rect_touches(tx0, tx1, ty0, ty1);
+    }
+    uint32_t t;
+    const uint32_t ex = block_exscan(cnt, s_tmp, &t);
+    if (g < a.n) a.pair_offset[g] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) partials[2 * nb + blockIdx.x] = carry;
 }
 
 // exclusive scan of the touch partials (single block); counters[0] = M, [1] = T
@@ -505,6 +537,15 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
     carry += tot;
     block_exscan(i < nb ? partials[nb + i] : 0u, s_tmp, &tot);
     vis += tot;
+  }
+  // index-order slot chunks (k_bin_partials): exclusive offsets in place
+  uint32_t slots = 0;
+  for (int c = 0; c < nb; c += kBlock) {
+    const int i = c + threadIdx.x;
+    const uint32_t v = i < nb ? partials[2 * nb + i] : 0u;
+    const uint32_t e = block_exscan(v, s_tmp, &tot);
+    if (i < nb) partials[2 * nb + i] = slots + e;
+    slots += tot;
   }
   if (threadIdx.x == 0) {
     counters[0] = vis;
@@ -539,10 +580,6 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
     s_g[threadIdx.x] = g;
     s_rect[threadIdx.x] = rc;
     if (threadIdx.x == 0) s_off[kBlock] = tot;
-    if (g != 0xFFFFFFFFu) {
-      a.pair_offset[g] = out_base + ex;
-      if (cnt) a.records[(size_t)g * GS_RECORD_FLOATS + 10] = __uint_as_float(out_base + ex);
-    }
     __syncthreads();
     for (uint32_t o = threadIdx.x; o < tot; o += kBlock) {
       // last i with s_off[i] <= o (entries with zero touches share offsets)
@@ -560,6 +597,19 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
       a.pair_gauss[out_base + o] = s_g[lo];
     }
     out_base += tot;
+  }
+  // Gradient slots, in Gaussian-index order over this block's index chunk
+  // (coalesced): the chunk's offset + each Gaussian's prefix in the chunk
+  // (k_bin_partials); the first slot is also kept in the record (word 10) for
+  // the backward.  Records of culled Gaussians are never read.
+  const uint32_t cbase = partials[2 * gridDim.x + blockIdx.x];
+  for (int r = 0; r < kBinChunk / kBlock; ++r) {
+    const long long g = base + r * kBlock + threadIdx.x;
+    if (g < a.n) {
+      const uint32_t slot = cbase + a.pair_offset[g];
+      a.pair_offset[g] = slot;
+      a.records[(size_t)g * GS_RECORD_FLOATS + 10] = __uint_as_float(slot);
+    }
   }
 }
 
@@ -707,10 +757,11 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         const float dx = fx - pm.x, dy = fy - pm.y;
         const float s = conic_s(dx, dy, pq.x, pq.y, po.x);  // :333
         // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp
-        const bool live = A < kAlphaStop && !(s > 23.1f);
+        const bool run = A < kAlphaStop;  // the pixel has not terminated
+        const bool live = run && !(s > 23.1f);
         if (wave_any(live)) {
           livem |= 1ull << bit;
-          const float w = sat01(exp_inrange(-0.5f * s));  // :334
+          const float w = sat01(exp_neg_half(s));  // :334
           // :336 / :340 / :345 skips folded into the weight: a skipped pair
           // gets ai = 0, hence c = (1 - A) * 0 = +0 (1 - A >= 0), and an
           // accepted one c = (1 - A) * ai > 0 -- the reference's c exactly.
@@ -718,14 +769,18 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
           const float ai = (live && !(w < kMinWeight)) ? sat01(po.y * w) : 0.f;  // :339
           const float c = (1.f - A) * ai;                                        // :343-344
           const float2 prg = lds_pair(&s_rec[6 * j + 3]), pbz = lds_pair(&s_rec[6 * j + 4]);
-          const float A0 = A;
-          ar += c * prg.x;
-          ag += c * prg.y;
-          ab += c * pbz.x;
+          // colour / depth sums fused (one rounding per term): they decide
+          // nothing -- termination reads A only -- and the backward reads
+          // their totals
+          ar = __builtin_fmaf(c, prg.x, ar);
+          ag = __builtin_fmaf(c, prg.y, ag);
+          ab = __builtin_fmaf(c, pbz.x, ab);
           A = A + c;
-          D += c * pbz.y;
-          // :352 (after accumulation): the lane's terminating entry
-          neval = (A0 < kAlphaStop && A >= kAlphaStop) ? b - start + j + 1 : neval;
+          D = __builtin_fmaf(c, pbz.y, D);
+          // :352 (after accumulation): the terminating entry is the last one
+          // reached while the pixel still ran (A only grows; a pixel still
+          // running at the end of its list gets end - start below)
+          neval = run ? b - start + j + 1 : neval;
         }
       }
       // (only words inside the tile's list: the next tile's words follow)
@@ -755,61 +810,82 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
 }
 
 // ======================================================== blend bwd =======
-// Two phases per batch of kBwdBatch list entries, so that no per-pair
-// cross-lane reduction is needed:
-//  A (pixel-parallel): every pixel replays its front-to-back chain over the
-//    batch -- bit-identical to the forward's decisions -- and writes two
-//    scalars per (entry, pixel) to LDS: dop = dL/d opacity and the
-//    contribution weight c, whose sign bit flags "exp(-s/2) <= 1" (then
-//    dL/ds = -0.5 * opacity * dop; otherwise the weight clamp blocks it).
-//  B (entry-parallel): each 16-lane row owns one entry, sums its 256 pixels
-//    (16 per lane) into the 10 gradient values, reduces the row with DPP and
-//    writes the entry's slot.
-#ifndef GS_BWD_BATCH
-#define GS_BWD_BATCH 16
-#endif
-constexpr int kBwdBatch = GS_BWD_BATCH;        // entries per batch: 8 or 16
-constexpr int kRowsPerEntry = 16 / kBwdBatch;  // 16-lane DPP rows summing one entry
-constexpr int kPdStride = kBlock + 16;  // rows of the pair arrays: +16 floats keeps 16-lane rows on disjoint banks
+// One 64-lane workgroup per (tile, 8x8 quadrant); lane = pixel, as in the
+// forward's waves.  Nothing couples the four quadrants of a tile (no
+// barrier): each walks only the list entries its own pixels evaluated in the
+// forward (the liveness bitmap, exact), in list order, and writes one partial
+// gradient per (entry, quadrant); gs_project_backward sums a slot's quadrant
+// partials.
+//  A (pixel-parallel), per live entry: replay the pixel's front-to-back chain
+//    -- bit-identical to the forward's decisions -- and put two scalars per
+//    pixel into a group buffer: dop = dL/d opacity and the contribution
+//    weight c, whose sign bit flags exp(-s/2) > 1 (the weight clamp then
+//    blocks dL/ds).
+//  B (entry-parallel), once per kBwdGroup live entries: lanes 8j..8j+7 sum
+//    entry j's 64 pixels -- lane 8j + x takes column x, rows 0..7 -- into the
+//    10 gradient values and reduce them with 3 DPP steps.
+// The records of a 64-entry word's live entries are gathered lane-parallel
+// one word ahead (registers), staged in LDS and read back as broadcasts.
+constexpr int kBwdGroup = 8;  // live entries per phase-B group
+// Group buffer rows (dop, c) are padded to 72 float2: phase B's lanes 8j + x
+// read row j at pixel x + 8r, and 72 puts rows j = 0..3 of a 32-lane half on
+// distinct banks (a stride of 64 would be a 4-way conflict).
+constexpr int kBwdRow = kWave + 8;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
-// Sum over the 16 lanes of each DPP row; every lane of the row gets the sum.
-__device__ __forceinline__ float row16_sum(float v) {
+// Sum over the 8 lanes 8j..8j+7 (a DPP half row); each of them gets the sum.
+__device__ __forceinline__ float oct_sum(float v) {
   v += dpp_row<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_row<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_row<0x124>(v);  // row_ror:4
-  v += dpp_row<0x128>(v);  // row_ror:8
+  v += dpp_row<0x141>(v);  // row_half_mirror: lane x <- lane 7 - x of its 8
   return v;
 }
 
-// Occupancy: the LDS footprint (~39 KB) allows 4 blocks per CU, i.e. 4 waves
-// per SIMD, which needs <= 128 VGPRs (phase B's unroll sets the peak).
-__global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
-  __shared__ float2 s_rec[2][kBwdBatch * 6];  // double-buffered: batch i+1 is staged during phase B(i)
-  __shared__ uint32_t s_e[2][kBwdBatch];
-  __shared__ float s_dop[kBwdBatch][kPdStride], s_c[kBwdBatch][kPdStride];
-  __shared__ float4 s_pg[kBlock];   // per pixel: dL/drgb (masked), dL/dD
-  __shared__ uint32_t s_max;
-  const int tile = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  int px, py;
-  tile_pixel(tile, a.tiles_x, px, py);
+// An entry whose clamps provably never bind: opacity in [1e-20, 1] and a
+// conic passing quad_mask's conditioning test (positive definite, fp32 s >= 0
+// at every pixel).  Then exp(-s/2) <= 1 and o w <= 1, and an accepted pair
+// has c = (1 - A) o w >= 0.005 * 1e-20 * 1e-5 > 0.
+__device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
+  const float q00 = r0.z, qo = r0.w, q11 = r1.x, o = r1.y;
+  const float q01 = 0.5f * qo;
+  const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
+  return o >= 1e-20f && o <= 1.f && tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det;
+}
+
+// Workgroup b -> (tile, quadrant): b, b+8, b+16, b+24 share an XCD (round-
+// robin dispatch; placement is for speed only), so the four quadrants of a
+// tile read its records through one L2.  Grid: ceil(tiles / 8) * 32.
+__device__ __forceinline__ void quad_tile(int &tile, int &quad) {
+  const uint32_t b = blockIdx.x;
+  quad = (int)((b >> 3) & 3u);
+  tile = (int)((b >> 5) * 8u + (b & 7u));
+}
+
+__global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
+  __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
+  __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
+  __shared__ float4 s_gi[kBwdGroup][2];  // group entry: (mx, my, q00, qo), (q11, -o/2, slot bits, 0)
+  __shared__ float2 s_wrec[kWave * 6];   // the word's live records; word 10 = the entry's slot
+  int tile, quad;
+  quad_tile(tile, quad);
+  if (tile >= a.tiles_x * a.tiles_y) return;
+  const int lane = threadIdx.x;
+  const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
+  const int x0 = (int)tx * GS_TILE + ((quad & 1) << 3), y0 = (int)ty * GS_TILE + ((quad >> 1) << 3);
+  const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
   const int W = a.cam.image_width, H = a.cam.image_height;
   const bool inside = px < W && py < H;
-  const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]),
-                 end = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
+  const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]);
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
-  if (tid == 0) s_max = 0;
   // pixel cotangents through clamp / bg composite / depth normalisation
   float gR0 = 0.f, gR1 = 0.f, gR2 = 0.f, gA = 0.f, gD = 0.f;
   float tr = 0.f, tg = 0.f, tbl = 0.f, Dt = 0.f, At = 0.f;
   uint32_t neval = 0;
-  const size_t HW = (size_t)W * H;
   if (inside) {
+    const size_t HW = (size_t)W * H;
     const size_t p = (size_t)py * W + px;
     const float4 acc = reinterpret_cast<const float4 *>(a.pix_acc)[p];
     const float2 st = reinterpret_cast<const float2 *>(a.pix_state)[p];
@@ -828,91 +904,156 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
       gA += -a.g_depth[p] * Dt / (den * den);
     }
   }
-  const float fx = (float)px, fy = (float)py;
-  s_pg[tid] = make_float4(gR0, gR1, gR2, gD);
-  __syncthreads();
-  // this wave's last evaluated entry, and the tile's
+  // the quadrant's last evaluated entry: nothing past it carries gradient here
   const uint32_t wstop = __builtin_amdgcn_readfirstlane(wave_max_u32(neval));
-  if ((tid & 63) == 0 && wstop) atomicMax(&s_max, wstop);
-  __syncthreads();
-  const uint32_t stop = start + __builtin_amdgcn_readfirstlane(s_max);  // uniform: scalar loop bounds
+  if (wstop == 0) return;
+  s_pg[lane] = make_float4(gR0, gR1, gR2, gD);
+  const float fx = (float)px, fy = (float)py;
   const float onemA = 1.f - At;
   // Suffix sums without per-channel state: with X_i = gR . col_i + gD z_i,
   //   sum_k gR_k (accT_k - acc_k) + gD (Dt - D) = K - P,
   //   K = gR . accT + gD Dt (per pixel),  P = gR . acc + gD D (running; acc starts at bg)
+  // and dL/dalpha_i = T_i (X_i + (P - K + gA (1 - At)) / T_{i+1}) = T_i (X_i + (P + G0) / T_{i+1}).
   const float K = (gR0 * tr + gR1 * tg) + (gR2 * tbl + gD * Dt);
+  const float G0 = __builtin_fmaf(gA, onemA, -K);
   float P = (gR0 * bg0 + gR1 * bg1) + gR2 * bg2;
   float A = 0.f;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
-  // phase B: 16-lane row r = tid >> 4 works on entry r / kRowsPerEntry, pixel groups k = part (mod kRowsPerEntry)
-  const int jj = (tid >> 4) / kRowsPerEntry, part = (tid >> 4) % kRowsPerEntry, sub = tid & 15;
-  // batch i+1's records are gathered into registers (threads < kBwdBatch)
-  // while batch i is processed; lds_barrier() keeps those loads in flight
-  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
-  if (tid < kBwdBatch && start + tid < stop) {
-    const uint32_t gid = a.sorted_gauss[start + tid];
-    n0 = recs[3 * (size_t)gid];
-    n1 = recs[3 * (size_t)gid + 1];
-    n2 = recs[3 * (size_t)gid + 2];
-  }
-  const uint32_t tile_x = (uint32_t)(tile % a.tiles_x), tile_y = (uint32_t)(tile / a.tiles_x);
-  // Staging of a batch (threads < kBwdBatch): records into LDS and each
-  // entry's emit index, pair_offset[g] + the tile's index in g's rectangle.
-  auto stage = [&](int buf) {
-    if (tid < kBwdBatch) {
-      float4 *d = reinterpret_cast<float4 *>(&s_rec[buf][6 * tid]);
-      d[0] = n0;
-      d[1] = n1;
-      d[2] = n2;
-      const uint32_t info = __float_as_uint(n2.w);
-      s_e[buf][tid] = __float_as_uint(n2.z) + (tile_y - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
-                      (tile_x - (info & 0xFFFu));
+  const unsigned long long *lw =
+      reinterpret_cast<const unsigned long long *>(a.live_bits) + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile;
+  const uint32_t nwords = (wstop + 63u) >> 6;
+  // liveness word wd of this quadrant, cut at wstop (bits past it were never written)
+  auto live_word = [&](uint32_t wd) -> unsigned long long {
+    const unsigned long long w = lw[wd];
+    // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+    const unsigned long long m =
+        ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)w);
+    const uint32_t rem = wstop - 64u * wd;
+    return rem < 64u ? m & ((1ull << rem) - 1ull) : m;
+  };
+  float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+  // lane l gathers the record of entry 64 wd + l when that entry is live here
+  auto fetch = [&](uint32_t wd, unsigned long long m) {
+    if ((m >> lane) & 1ull) {
+      const uint32_t gid = a.sorted_gauss[start + 64u * wd + (uint32_t)lane];
+      r0 = recs[3 * (size_t)gid];
+      r1 = recs[3 * (size_t)gid + 1];
+      r2 = recs[3 * (size_t)gid + 2];
     }
   };
-  auto prefetch = [&](uint32_t bn) {
-    if (tid < kBwdBatch && bn + tid < stop) {
-      const uint32_t gid = a.sorted_gauss[bn + tid];
-      n0 = recs[3 * (size_t)gid];
-      n1 = recs[3 * (size_t)gid + 1];
-      n2 = recs[3 * (size_t)gid + 2];
-    }
-  };
-  stage(0);
-  prefetch(start + kBwdBatch);
-  lds_barrier();
-  // Two barriers per batch: A(i) | X | stage(i+1) + B(i) | Y | A(i+1) ...
-  // Y orders B(i)'s reads of s_dop/s_c before A(i+1)'s writes and makes the
-  // staged batch visible; s_rec[buf^1] was last read by B(i-1), before X.
-  int buf = 0;
-  for (uint32_t b = start; b < stop; b += kBwdBatch, buf ^= 1) {
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(min((uint32_t)kBwdBatch, stop - b));
-    // ---- phase A: replay ------------------------------------------------
-    const uint32_t jbase = b - start;
-    // entries this wave replays: the forward's liveness bits of its quadrant
-    // (64 % kBwdBatch == 0: a batch never straddles two words), cut at the
-    // wave's last evaluated entry (bits past it were never written); the
-    // other entries only store zeros
-    const uint32_t lim = wstop > jbase ? min(wstop - jbase, 32u) : 0u;
-    uint32_t qw = 0;
-    if (lim) {
-      const unsigned long long lw = a.live_bits[(size_t)wave * a.live_words + start / 64u + (uint32_t)tile + jbase / 64u];
-      const uint32_t bits = (uint32_t)(lw >> (jbase & 63u)) & ((1u << kBwdBatch) - 1u);
-      qw = __builtin_amdgcn_readfirstlane(bits) & (lim >= 32u ? ~0u : ((1u << lim) - 1u));
-    }
-    for (uint32_t j = 0; j < cnt; ++j) {
-      float dop = 0.f, cw = 0.f;
-      if (!((qw >> j) & 1u)) {
-        s_dop[j][tid] = 0.f;
-        s_c[j][tid] = 0.f;
-        continue;
+  int k = 0;             // entries in the group buffer (wave-uniform)
+  uint32_t gsimple = 0;  // bit j: group entry j is simple_entry, so phase B needs no clamp mask
+  auto phase_b = [&](auto masked_tag) {
+    constexpr bool kMasked = decltype(masked_tag)::value;
+    // this wave's group writes have landed before other lanes read them
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int j = lane >> 3, col = lane & 7;
+    if (j < k) {
+      const float4 ia = s_gi[j][0], ib = s_gi[j][1];
+      const float hop = ib.y;
+      // this lane's pixels (x0 + col, y0 + r), r = 0..7: dx = bx, dy = by + r
+      const float bx = (float)(x0 + col) - ia.x, by = (float)y0 - ia.y;
+      float S0 = 0.f, Soy = 0.f, Soyy = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int p = col + 8 * r;  // phase A's lane of that pixel
+        const float2 dc = s_dc[j][p];
+        const float dop = dc.x, cs = dc.y;
+        const float4 pg = s_pg[p];
+        // dL/ds: none where the weight clamp bound (sign bit of c) or the pair
+        // was skipped (dop = 0 then); a simple entry's clamps never bind
+        const float ds = kMasked ? (cs > 0.f ? hop * dop : 0.f) : hop * dop;
+        const float cw = fabsf(cs);
+        S0 += ds;
+        if (r) {
+          Soy = __builtin_fmaf(ds, (float)r, Soy);
+          Soyy = __builtin_fmaf(ds, (float)(r * r), Soyy);
+        }
+        g5 += dop;
+        g6 = __builtin_fmaf(pg.x, cw, g6);
+        g7 = __builtin_fmaf(pg.y, cw, g7);
+        g8 = __builtin_fmaf(pg.z, cw, g8);
+        g9 = __builtin_fmaf(pg.w, cw, g9);
       }
-      const float2 pm = lds_pair(&s_rec[buf][6 * j]), pq = lds_pair(&s_rec[buf][6 * j + 1]),
-                   po = lds_pair(&s_rec[buf][6 * j + 2]);
+      // sums of ds dx, ds dy, ds dx^2, ds dx dy, ds dy^2 over the lane's column
+      float Sx = bx * S0, Sy = __builtin_fmaf(by, S0, Soy);
+      float g2 = bx * Sx, g3 = bx * Sy;
+      float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
+      Sx = oct_sum(Sx); Sy = oct_sum(Sy); g2 = oct_sum(g2); g3 = oct_sum(g3); g4 = oct_sum(g4);
+      g5 = oct_sum(g5); g6 = oct_sum(g6); g7 = oct_sum(g7); g8 = oct_sum(g8); g9 = oct_sum(g9);
+      if (col == 0) {
+        const float q00 = ia.z, qo = ia.w, q11 = ib.x;
+        // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
+        const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
+        const size_t e = (size_t)__float_as_uint(ib.z) * 4u + (uint32_t)quad;
+        float2 *out = reinterpret_cast<float2 *>(a.pair_grads + e * GS_PAIR_GRAD_FLOATS);
+        out[0] = make_float2(g0, g1);
+        out[1] = make_float2(g2, g3);
+        out[2] = make_float2(g4, g5);
+        out[3] = make_float2(g6, g7);
+        out[4] = make_float2(g8, g9);
+        a.slot_live[e] = 1;
+      }
+    }
+    k = 0;
+    gsimple = 0;
+  };
+  unsigned long long mcur = live_word(0);
+  fetch(0, mcur);
+  for (uint32_t wd = 0; wd < nwords; ++wd) {
+    // stage the word's live records; word 10 becomes the entry's gradient
+    // slot (the Gaussian's first slot + this tile's index in its rectangle)
+    const bool mine = (mcur >> lane) & 1ull;
+    if (mine) {
+      const uint32_t info = __float_as_uint(r2.w);
+      const uint32_t slot = __float_as_uint(r2.z) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
+                            (tx - (info & 0xFFFu));
+      float4 *d = reinterpret_cast<float4 *>(&s_wrec[6 * lane]);
+      d[0] = r0;
+      d[1] = r1;
+      d[2] = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
+    }
+    const unsigned long long simple_w = __builtin_amdgcn_ballot_w64(mine && simple_entry(r0, r1));
+    const unsigned long long mnext = wd + 1u < nwords ? live_word(wd + 1u) : 0ull;
+    fetch(wd + 1u, mnext);  // in flight while this word replays
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
+    unsigned long long m = mcur;
+    while (m) {
+      const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1ull;
+      const uint32_t i = 64u * wd + bit;
+      // two b128 broadcasts and a b64: (mx my q00 qo) (q11 o r g) (b z)
+      const float4 r0v = reinterpret_cast<const float4 *>(s_wrec)[3 * bit];
+      const float4 r1v = reinterpret_cast<const float4 *>(s_wrec)[3 * bit + 1];
+      const float2 pbz = s_wrec[6 * bit + 4];
+      const float2 pm = make_float2(r0v.x, r0v.y), pq = make_float2(r0v.z, r0v.w);
+      const float2 po = make_float2(r1v.x, r1v.y), prg = make_float2(r1v.z, r1v.w);
       const float dx = fx - pm.x, dy = fy - pm.y;
       const float sq = conic_s(dx, dy, pq.x, pq.y, po.x);
       // exp(-11.55) < 1e-5: exact early skip (NaN falls through), as in the forward
-      const bool live = (jbase + j < neval) && !(sq > 23.1f);
-      if (wave_any(live)) {
+      const bool live = (i < neval) && !(sq > 23.1f);
+      const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
+      const bool simple = (simple_w >> bit) & 1ull;
+      float dop, cw;
+      if (simple) {
+        // Fast path (simple_entry): e = exp(-s/2) lies in [0, 1] (s >= 0) and
+        // u = o w in [0, 1], so both clamps are identities and pass their
+        // gradients -- the general path below with its clamp tests removed,
+        // the same values.  wv = 0 exactly where the pair is skipped.
+        const float w = exp_neg_half(sq);
+        const float wv = (live && !(w < kMinWeight)) ? w : 0.f;
+        const float trans = 1.f - A;
+        const float c = trans * (po.y * wv);
+        A = A + c;
+        P = __builtin_fmaf(c, X, P);
+        const float inv = __builtin_amdgcn_rcpf(1.f - A);  // v_rcp_f32 (1 ulp): a gradient factor, no decision
+        const float d_live = __builtin_fmaf(inv, P + G0, X);
+        // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
+        const float dal = trans * (A >= kAlphaStop ? X + gA : d_live);
+        dop = dal * wv;
+        cw = c;
+      } else {
         const float e = exp_inrange(-0.5f * sq);
         const float w = sat01(e);
         const float u = po.y * w;
@@ -921,110 +1062,71 @@ __global__ __launch_bounds__(kBlock) void k_blend_bwd(gs_blend_bwd_args a) {
         // the forward's skips folded into the weight exactly as there: c is
         // +0 for a skipped pair and > 0 for an accepted one (take <=> c > 0)
         const float c = trans * ((live && !(w < kMinWeight)) ? ai : 0.f);
-        const float2 prg = lds_pair(&s_rec[buf][6 * j + 3]), pbz = lds_pair(&s_rec[buf][6 * j + 4]);
-        const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
         A = A + c;
         P = __builtin_fmaf(c, X, P);
-        // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
         const bool term = A >= kAlphaStop;
         // both arms computed, then a select: no divergent branch per entry
-        const float inv = __builtin_amdgcn_rcpf(1.f - A);  // v_rcp_f32 (1 ulp): a gradient factor, no decision
-        const float d_live = __builtin_fmaf(inv, __builtin_fmaf(gA, onemA, P - K), X);
-        const float d_term = X + gA;
-        const float dal = trans * (term ? d_term : d_live);
+        const float inv = __builtin_amdgcn_rcpf(1.f - A);
+        const float d_live = __builtin_fmaf(inv, P + G0, X);
+        const float dal = trans * (term ? X + gA : d_live);
         // u = o*w >= 0, so "u in [0,1]" (the clamp passes the gradient) is ai == u;
         // e = exp(.) >= 0, so "e in [0,1]" is w == e (both false for NaN)
         const float g = (ai == u) ? dal * w : 0.f;
         dop = (c > 0.f) ? g : 0.f;
         cw = (w == e) ? c : -c;  // c == +0 when skipped
       }
-      s_dop[j][tid] = dop;
-      s_c[j][tid] = cw;
-    }
-    lds_barrier();  // X
-    stage(buf ^ 1);
-    prefetch(b + 2 * kBwdBatch);
-    // ---- phase B: per-entry sums ----------------------------------------
-    if ((uint32_t)jj < cnt) {
-      const float2 pm = s_rec[buf][6 * jj], pq = s_rec[buf][6 * jj + 1], po = s_rec[buf][6 * jj + 2];
-      const float mx = pm.x, my = pm.y, hop = -0.5f * po.y;
-      // pixel p = sub + 16k sits at (tile_x0 + 8((k>>2)&1) + (sub&7), tile_y0 + 8(k>>3) + 2(k&3) + (sub>>3))
-      const float bx = (float)((tile % a.tiles_x) * GS_TILE + (sub & 7)) - mx;
-      const float by = (float)((tile / a.tiles_x) * GS_TILE + (sub >> 3)) - my;
-      // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy) with Sx = sum ds dx, Sy = sum ds dy.
-      // A lane's 16 pixels sit at (bx + ox_k, by + oy_k) with compile-time
-      // offsets ox_k in {0, 8}, oy_k in {0, 2, .., 14}: the sums over them of
-      // ds dx, ds dx^2, ds dx dy, .. are formed from sums of ds times the
-      // constant offsets (S0, Sox, Soxx, ..; zero offsets cost nothing), then
-      // expanded once per lane with bx, by.
-      float S0 = 0.f, Sox = 0.f, Soy = 0.f, Soxx = 0.f, Soxy = 0.f, Soyy = 0.f;
-      float g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 16 / kRowsPerEntry; ++kk) {
-        const int k = part + kRowsPerEntry * kk;
-        const int p = sub + 16 * k;
-        const float dop = s_dop[jj][p], cs = s_c[jj][p];
-        const float4 pg = s_pg[p];
-        const int ox = 8 * ((k >> 2) & 1), oy = 8 * (k >> 3) + 2 * (k & 3);
-        const float cw = fabsf(cs);
-        const float ds = cs > 0.f ? hop * dop : 0.f;
-        S0 += ds;
-        if (ox) {
-          Sox = __builtin_fmaf(ds, (float)ox, Sox);
-          Soxx = __builtin_fmaf(ds, (float)(ox * ox), Soxx);
-        }
-        if (oy) {
-          Soy = __builtin_fmaf(ds, (float)oy, Soy);
-          Soyy = __builtin_fmaf(ds, (float)(oy * oy), Soyy);
-        }
-        if (ox && oy) Soxy = __builtin_fmaf(ds, (float)(ox * oy), Soxy);
-        g5 += dop;
-        g6 = __builtin_fmaf(pg.x, cw, g6);
-        g7 = __builtin_fmaf(pg.y, cw, g7);
-        g8 = __builtin_fmaf(pg.z, cw, g8);
-        g9 = __builtin_fmaf(pg.w, cw, g9);
-        // keep the second half's LDS reads below this point: hoisting all 48
-        // of them needs > 128 VGPRs (fewer than 4 waves per SIMD)
-        if (kk == 7) __builtin_amdgcn_sched_barrier(0);
+      s_dc[k][lane] = make_float2(dop, cw);
+      if (lane == 0) {
+        const float2 ps = s_wrec[6 * bit + 5];
+        s_gi[k][0] = make_float4(pm.x, pm.y, pq.x, pq.y);
+        s_gi[k][1] = make_float4(po.x, -0.5f * po.y, ps.x, 0.f);
       }
-      float Sx = __builtin_fmaf(bx, S0, Sox), Sy = __builtin_fmaf(by, S0, Soy);
-      float g2 = __builtin_fmaf(bx, __builtin_fmaf(bx, S0, 2.f * Sox), Soxx);
-      float g3 = __builtin_fmaf(bx, __builtin_fmaf(by, S0, Soy), __builtin_fmaf(by, Sox, Soxy));
-      float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
-      Sx = row16_sum(Sx); Sy = row16_sum(Sy); g2 = row16_sum(g2); g3 = row16_sum(g3); g4 = row16_sum(g4);
-      g5 = row16_sum(g5); g6 = row16_sum(g6); g7 = row16_sum(g7); g8 = row16_sum(g8); g9 = row16_sum(g9);
-      if (kRowsPerEntry == 2) {  // rows 2i, 2i+1 of a wave hold halves of one entry
-        Sx += __shfl_xor(Sx, 16); Sy += __shfl_xor(Sy, 16); g2 += __shfl_xor(g2, 16); g3 += __shfl_xor(g3, 16);
-        g4 += __shfl_xor(g4, 16); g5 += __shfl_xor(g5, 16); g6 += __shfl_xor(g6, 16); g7 += __shfl_xor(g7, 16);
-        g8 += __shfl_xor(g8, 16); g9 += __shfl_xor(g9, 16);
-      }
-      if (sub == 0 && part == 0) {
-        const float q00 = pq.x, qo = pq.y, q11 = po.x;
-        const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
-        float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)s_e[buf][jj] * GS_PAIR_GRAD_FLOATS);
-        out[0] = make_float2(g0, g1);
-        out[1] = make_float2(g2, g3);
-        out[2] = make_float2(g4, g5);
-        out[3] = make_float2(g6, g7);
-        out[4] = make_float2(g8, g9);
+      gsimple |= (uint32_t)simple << k;
+      if (++k == kBwdGroup) {
+        if (gsimple == (1u << kBwdGroup) - 1u) phase_b(std::false_type{}); else phase_b(std::true_type{});
       }
     }
-    lds_barrier();  // Y
+    mcur = mnext;
   }
-  // entries past every pixel's last evaluated pair carry no gradient
-  const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
-  for (uint32_t q = stop + tid; q < end; q += kBlock) {
-    const uint32_t gid = a.sorted_gauss[q];
-    const float w7 = a.records[(size_t)gid * GS_RECORD_FLOATS + 10];
-    const uint32_t info = __float_as_uint(a.records[(size_t)gid * GS_RECORD_FLOATS + 11]);
-    const uint32_t e = __float_as_uint(w7) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) + (tx - (info & 0xFFFu));
-    float2 *out = reinterpret_cast<float2 *>(a.pair_grads + (size_t)e * GS_PAIR_GRAD_FLOATS);
-#pragma unroll
-    for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) out[k] = make_float2(0.f, 0.f);
+  if (k) {
+    if (gsimple == (1u << k) - 1u) phase_b(std::false_type{}); else phase_b(std::true_type{});
   }
 }
 
 // ======================================================== project bwd =====
+// Sum of each slot's quadrant partials: 4 lanes per slot (lane q reads
+// quadrant q's partial where slot_live flags it), added in a fixed DPP order
+// -- bitwise reproducible.  Slot-major, so a wave's loads cover one
+// contiguous run of slots (coalesced); the slot sums are then read by
+// k_project_bwd per Gaussian, whose slots are consecutive.
+__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) {
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long e = t >> 2;
+  const int q = (int)(t & 3);
+  constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
+  float2 v[kF2];
+#pragma unroll
+  for (int k = 0; k < kF2; ++k) v[k] = make_float2(0.f, 0.f);
+  if (e < a.num_slots && a.slot_live[t]) {
+    const float2 *src = reinterpret_cast<const float2 *>(a.pair_grads) + (size_t)t * kF2;
+#pragma unroll
+    for (int k = 0; k < kF2; ++k) v[k] = src[k];
+  }
+  // (p0 + p1) + (p2 + p3) on every lane of the quad
+#pragma unroll
+  for (int k = 0; k < kF2; ++k) {
+    v[k].x += dpp_row<0xB1>(v[k].x);
+    v[k].y += dpp_row<0xB1>(v[k].y);
+    v[k].x += dpp_row<0x4E>(v[k].x);
+    v[k].y += dpp_row<0x4E>(v[k].y);
+  }
+  if (q == 0 && e < a.num_slots) {
+    float2 *out = reinterpret_cast<float2 *>(a.slot_sums) + (size_t)e * kF2;
+#pragma unroll
+    for (int k = 0; k < kF2; ++k) out[k] = v[k];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   const int k = blockIdx.x * kBlock + threadIdx.x;
   if (k >= a.g.n) return;
@@ -1038,7 +1140,9 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
     unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
     const uint32_t cnt = rect_touches(tx0, tx1, ty0, ty1);
     const uint32_t off = a.pair_offset[g];
-    const float2 *sl = reinterpret_cast<const float2 *>(a.pair_grads + (size_t)off * GS_PAIR_GRAD_FLOATS);
+    // g's slot sums (k_gather_slots) are consecutive, and so are those of
+    // g + 1 (index-order slots): coalesced across the wave
+    const float2 *sl = reinterpret_cast<const float2 *>(a.slot_sums + (size_t)off * GS_PAIR_GRAD_FLOATS);
     constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
     uint32_t e = 0;
     // four slots' loads in flight per round trip (the summation order stays
@@ -1385,13 +1489,14 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
 }
 
 size_t gs_bin_workspace_bytes(int32_t n) {
-  return 2 * sizeof(uint32_t) * (size_t)(n > 0 ? div_up(n, kBinChunk) : 1) + 256;
+  return 3 * sizeof(uint32_t) * (size_t)(n > 0 ? div_up(n, kBinChunk) : 1) + 256;
 }
 
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
   if (!a || !a->counters) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_bin_count");
   if (a->n <= 0) return GS_OK;
-  if (!a->sorted_ids || !a->rects || !a->vis || !a->workspace || a->workspace_bytes < gs_bin_workspace_bytes(a->n))
+  if (!a->sorted_ids || !a->rects || !a->vis || !a->pair_offset || !a->workspace ||
+      a->workspace_bytes < gs_bin_workspace_bytes(a->n))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer or workspace too small", "gs_bin_count");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
@@ -1447,10 +1552,12 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (a->tiles_x != (int)div_up(a->cam.image_width, GS_TILE) || a->tiles_y != (int)div_up(a->cam.image_height, GS_TILE))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_backward");
   if (!a->ranges || !a->records || !a->pix_acc || !a->pix_state || !a->g_image || !a->pair_grads ||
-      !a->live_bits || a->live_words <= 0)
+      !a->slot_live || !a->live_bits || a->live_words <= 0)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_backward");
   hipStream_t s = (hipStream_t)stream;
-  k_blend_bwd<<<a->tiles_x * a->tiles_y, kBlock, 0, s>>>(*a);
+  const int num_tiles = a->tiles_x * a->tiles_y;
+  if (num_tiles <= 0) return GS_OK;
+  k_blend_bwd<<<div_up(num_tiles, 8) * 32u, kWave, 0, s>>>(*a);
   return check_launch("gs_blend_backward");
 }
 
@@ -1460,12 +1567,14 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   const bool raw = a->g.cov3d == nullptr;
   if (!a->g.xyz || !a->g.color_logits || !a->means2d || !a->conics || !a->vis || !a->rects ||
       !a->pair_offset || !a->d_xyz || !a->d_color_logits || !a->d_opacity ||
-      (raw ? (!a->g.scaling || !a->g.rotation || !a->d_scaling || !a->d_rotation) : !a->d_cov3d))
+      (raw ? (!a->g.scaling || !a->g.rotation || !a->d_scaling || !a->d_rotation) : !a->d_cov3d) ||
+      (a->pair_grads && (!a->slot_live || !a->slot_sums || a->num_slots < 0)))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_project_backward");
   if (a->g.sh_degree < 0 || a->g.sh_degree > 3 || (a->g.sh_degree > 0 && (!a->g.sh_rest || !a->d_sh_rest)))
     return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest and d_sh_rest when > 0",
                 "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
+  if (a->pair_grads && a->num_slots > 0) k_gather_slots<<<div_up(4LL * a->num_slots, kBlock), kBlock, 0, s>>>(*a);
   k_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_backward");
 }

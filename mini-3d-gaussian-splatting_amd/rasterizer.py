@@ -191,14 +191,14 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         sorted_ids = vals[alt.value]
         fr.order = sorted_ids
         bws = torch.empty((lib.gs_bin_workspace_bytes(n),), dtype=torch.uint8, device=dev)
+        pair_offset = torch.empty((n,), dtype=i32, device=dev)
         ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(vis),
-                         N.ptr(counters), N.ptr(bws), bws.numel(), 0, 0, 0, N.ptr(records))
+                         N.ptr(counters), N.ptr(bws), bws.numel(), 0, 0, N.ptr(pair_offset), N.ptr(records))
         StageTimer.mark("bin_count")
         N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
         # everything whose size does not depend on T is allocated before the
         # one host sync, so the GPU waits only for the read-back and launches
         num_tiles = cam.tiles_x * cam.tiles_y
-        pair_offset = torch.empty((n,), dtype=i32, device=dev)
         ranges = torch.empty((num_tiles, 2), dtype=i32, device=dev)
         image = torch.empty((3, H, W), dtype=f32, device=dev)
         alpha = torch.empty((1, H, W), dtype=f32, device=dev)
@@ -238,7 +238,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     o_ws = (16 * cap_t + 255) // 256 * 256
     o_live = o_ws + (int(lib.gs_radix_sort_workspace_bytes(cap_t)) + 255) // 256 * 256
     p_ws, p_live = base + o_ws, base + o_live
-    ba.tile_keys, ba.pair_gauss, ba.pair_offset = p_tk[0], p_tv[0], N.ptr(pair_offset)
+    ba.tile_keys, ba.pair_gauss = p_tk[0], p_tv[0]
     StageTimer.mark("bin_emit")
     N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
 
@@ -270,14 +270,17 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
 
 def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotation, logits, opacity,
                       means2d, conics, g_image, g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit=False,
-                      sh_rest=None, sh_degree=0):
+                      sh_rest=None, sh_degree=0, out=None):
+    """out: optional preallocated gradient tensors {name: tensor} (the
+    data-parallel bucket's views, distributed.GradAllReduce.attach); the
+    kernels write there instead of into fresh buffers."""
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
     f32 = torch.float32
     s = _stream()
     cs = cam.to_struct()
-    pair_grads = None
+    pair_grads = slot_live = None
     pixel_grads = g_image is not None or g_alpha is not None or g_depth is not None
     if fr.M > 0 and fr.T > 0 and pixel_grads:
         if g_image is None:
@@ -285,29 +288,40 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_image = g_image.contiguous()
         g_alpha = None if g_alpha is None else g_alpha.contiguous()
         g_depth = None if g_depth is None else g_depth.contiguous()
-        pair_grads = torch.empty((max(fr.T, 1), N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
+        # one partial per (slot, 8x8 quadrant); only the quadrants that replay
+        # an entry write theirs and set its flag
+        pair_grads = torch.empty((fr.T * 4, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
+        slot_live = torch.zeros((fr.T * 4,), dtype=torch.uint8, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
-                              fr.live_bits.shape[1], N.ptr(pair_grads))
+                              fr.live_bits.shape[1], N.ptr(pair_grads), N.ptr(slot_live))
         StageTimer.mark("blend_bwd")
         N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
     raw = cov3d is None
-    d_xyz = torch.empty((n, 3), dtype=f32, device=dev)
+    out = out or {}
+
+    def buf(name, shape):
+        t = out.get(name)
+        return t.view(shape) if t is not None else torch.empty(shape, dtype=f32, device=dev)
+    d_xyz = buf("xyz", (n, 3))
     d_cov = None if raw else torch.empty((n, 3, 3), dtype=f32, device=dev)
-    d_scl = torch.empty((n, 3), dtype=f32, device=dev) if raw else None
-    d_rot = torch.empty((n, 4), dtype=f32, device=dev) if raw else None
-    d_col = torch.empty((n, 3), dtype=f32, device=dev)
-    d_op = torch.empty((n,), dtype=f32, device=dev)
+    d_scl = buf("scaling", (n, 3)) if raw else None
+    d_rot = buf("rotation", (n, 4)) if raw else None
+    d_col = buf("color", (n, 3))
+    d_op = buf("opacity", (n,))
     gm = None if g_means2d is None else g_means2d.contiguous()
     gc = None if g_conics is None else g_conics.contiguous()
-    d_sh = torch.empty((n, N.GS_SH_REST, 3), dtype=f32, device=dev) if sh_degree > 0 else None
+    d_sh = buf("sh_rest", (n, N.GS_SH_REST, 3)) if sh_degree > 0 else None
     gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
+    slot_sums = None if pair_grads is None else torch.empty((fr.T, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
     pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
                             # Gaussian order (order=NULL): inputs/outputs stream; walking in depth
                             # order coalesces the slot reads but scatters 10 arrays (measured 2.4x slower)
                             N.ptr(fr.pair_offset), None, N.ptr(pair_grads), N.ptr(gm), N.ptr(gc), N.ptr(d_xyz),
-                            N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op), N.ptr(d_sh))
+                            N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op), N.ptr(d_sh),
+                            N.ptr(slot_live), N.ptr(slot_sums),
+                            fr.T if pair_grads is not None else 0)
     StageTimer.mark("project_bwd")
     N.check(lib.gs_project_backward(C.byref(pb), s), "gs_project_backward")
     StageTimer.mark("~end_bwd")
@@ -320,10 +334,11 @@ class RasterizeGaussians(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, cam: CameraParams,
-                opacity_is_logit=False, sh_degree=0):
+                opacity_is_logit=False, sh_degree=0, grad_dest=None):
         image, alpha, depth, means2d, conics, radii, vis, fr = forward_pipeline(
             cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
         ctx.cam, ctx.frame, ctx.opacity_is_logit, ctx.sh_degree = cam, fr, opacity_is_logit, sh_degree
+        ctx.grad_dest = grad_dest
         ctx.save_for_backward(xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics)
         ctx.mark_non_differentiable(radii, vis)
         ctx.set_materialize_grads(False)
@@ -333,10 +348,11 @@ class RasterizeGaussians(torch.autograd.Function):
     def backward(ctx, g_image, g_alpha, g_depth, g_means2d, g_conics, _g_radii, _g_vis):
         xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics = ctx.saved_tensors
         g_conics = None if g_conics is None else g_conics.reshape(-1, 4)
+        dest = ctx.grad_dest() if ctx.grad_dest is not None else None
         d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh = backward_pipeline(
             ctx.cam, ctx.frame, xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics,
             g_image, None if g_alpha is None else g_alpha, g_depth, g_means2d, g_conics, ctx.opacity_is_logit,
-            sh_rest, ctx.sh_degree)
+            sh_rest, ctx.sh_degree, out=dest)
         need = ctx.needs_input_grad
         return (d_xyz if need[0] else None,
                 d_cov if (cov3d is not None and need[1]) else None,
@@ -345,16 +361,19 @@ class RasterizeGaussians(torch.autograd.Function):
                 d_col if need[4] else None,
                 d_op.view(opacity.shape) if need[5] else None,
                 d_sh if (sh_rest is not None and need[6]) else None,
-                None, None, None)
+                None, None, None, None)
 
 
 def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
-              sh_rest=None, sh_degree=0):
+              sh_rest=None, sh_degree=0, grad_dest=None):
     """opacity_is_logit: opacity holds the model's raw _opacity and the kernels
     apply get_opacity's sigmoid (fused; its gradient goes to the logit).
     sh_degree > 0: view-dependent colour from sh_rest ([N,15,3] rest
     coefficients, e.g. get_features[:,1:,:]); 0 is the reference's DC-only
-    colour (include/gsplat_mi355x.h, gs_gaussians)."""
+    colour (include/gsplat_mi355x.h, gs_gaussians).
+    grad_dest: optional callable, asked at backward time, returning None or
+    {name: tensor} buffers the gradient kernels write into (names xyz,
+    scaling, rotation, color, opacity, sh_rest; see backward_pipeline)."""
     _check_inputs(xyz)
     sh_degree = int(sh_degree)
     if not 0 <= sh_degree <= 3:
@@ -377,4 +396,4 @@ def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity,
     logits, _ = _rows(logits, 3)
     opacity, _ = _rows(opacity, 1)
     return RasterizeGaussians.apply(xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, cam,
-                                    bool(opacity_is_logit), sh_degree)
+                                    bool(opacity_is_logit), sh_degree, grad_dest)

@@ -108,9 +108,24 @@ class GaussianRenderer:
         sh_rest = None
         if sh_degree > 0:
             sh_rest = gaussians._features_rest if fused else feats[:, 1:, :]
+        grad_dest = None
+        sink = getattr(gaussians, "_gs_grad_sink", None) if fused else None
+        if sink is not None:
+            # data-parallel bucket (distributed.GradAllReduce.attach): the
+            # gradient kernels write straight into it when it can take them
+            names = ["xyz", "color", "opacity", "scaling", "rotation"]
+            leaves = [gaussians._xyz, gaussians._features_dc, gaussians._opacity, gaussians._scaling,
+                      gaussians._rotation]
+            if sh_degree > 0:
+                names.append("sh_rest")
+                leaves.append(gaussians._features_rest)
+
+            def grad_dest():
+                views = sink.grad_destinations(leaves)
+                return None if views is None else dict(zip(names, views))
         image, alpha, depth, means2d, conics, radii, vis = rasterize(
             cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=fused,
-            sh_rest=sh_rest, sh_degree=sh_degree)
+            sh_rest=sh_rest, sh_degree=sh_degree, grad_dest=grad_dest)
         return {
             "image": image,
             "alpha": alpha,

@@ -100,7 +100,8 @@ class GaussianTrainer:
             params = g.grad_parameters()
             if self._reducer is None or self._reducer_n != g.get_num_points():
                 from .distributed import GradAllReduce
-                self._reducer, self._reducer_n = GradAllReduce(params, self._dist), g.get_num_points()
+                self._reducer = GradAllReduce(params, self._dist).attach(g)
+                self._reducer_n = g.get_num_points()
             self._reducer.params = params
             self._reducer.all_reduce_mean()
         opt.update_learning_rate(self.iteration)

@@ -62,3 +62,58 @@ def test_grad_all_reduce_mean_gloo():
         exp = (a + b) / 2
         assert torch.allclose(res[0][1][i], exp, atol=1e-6)
         assert torch.equal(res[0][1][i], res[1][1][i])  # replicas stay identical
+
+
+def _worker_zero_copy(rank, world, port, q):
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = pkg.GaussianModel()
+        m.create_from_random(50, generator=torch.Generator().manual_seed(0))
+        params = m.grad_parameters()
+        red = pkg.distributed.GradAllReduce(params, dist).attach(m)
+        assert m._gs_grad_sink is red
+        # what the render backward does: write into the bucket views, which
+        # autograd then adopts as the .grad tensors
+        dest = red.grad_destinations(params)
+        assert dest is not None and [d.shape for d in dest] == [p.shape for p in params]
+        g = torch.Generator().manual_seed(200 + rank)
+        for p, d in zip(params, dest):
+            d.copy_(torch.randn(p.shape, generator=g))
+            p.grad = d
+        local = [p.grad.clone() for p in params]
+        ptrs = [p.grad.data_ptr() for p in params]
+        assert red.grad_destinations(params) is None  # a .grad exists: the kernels need fresh buffers
+        red.all_reduce_mean()
+        assert [p.grad.data_ptr() for p in params] == ptrs  # reduced in place, no copies
+        q.put((rank, local, [p.grad.clone() for p in params]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_all_reduce_zero_copy_gloo():
+    """The backward writes into the bucket (GradAllReduce.attach): the mean is
+    formed in place and the .grad tensors stay views of the bucket."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_zero_copy, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict()
+    for _ in range(2):
+        r, local, reduced = q.get(timeout=120)
+        res[r] = (local, reduced)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i in range(len(res[0][0])):
+        exp = (res[0][0][i] + res[1][0][i]) / 2
+        assert torch.allclose(res[0][1][i], exp, atol=1e-6)
+        assert torch.equal(res[0][1][i], res[1][1][i])

@@ -331,3 +331,27 @@ def test_c3_full_size_vs_oracle(pkg, cuda):
     errs += G.check_grad("rotation", _np(m._rotation.grad), dr)
     errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"])
     assert not errs, errs
+
+
+def test_grad_bucket_adoption(pkg, cuda):
+    """GradAllReduce.attach (data-parallel path): the render backward writes
+    the gradients straight into the all-reduce bucket and autograd adopts the
+    views as .grad (no copies); the values equal a plain backward's."""
+    syn = pkg.synthetic
+    sc = syn.make_scene(20000, 320, 240, seed=3)
+    res = []
+    for attach in (False, True):
+        m = syn.to_model(sc, pkg.GaussianModel, cuda)
+        params = m.grad_parameters()
+        red = pkg.distributed.GradAllReduce(params, dist=object())  # no collective is issued here
+        if attach:
+            red.attach(m)
+        out = pkg.GaussianRenderer().render(Cam(320, 240, sc.fovx, sc.fovy), m,
+                                            pkg.RenderSettings(240, 320, torch.zeros(3)))
+        (out["image"].sum() + out["depth"].sum()).backward()
+        res.append([p.grad.clone() for p in params])
+        if attach:
+            for p, v in zip(params, torch.split(red._flat, red._sizes)):
+                assert p.grad.data_ptr() == v.data_ptr()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
