@@ -258,8 +258,7 @@ typedef struct gs_project_bwd_args {
   float *d_opacity;            /* [n]   */
   float *d_sh_rest;            /* [n,15,3] contiguous, written when g.sh_degree > 0 (zeros past the degree) */
   const uint8_t *slot_live;    /* [T,4] from gs_blend_backward; required with pair_grads */
-  float *slot_sums;            /* [T, GS_PAIR_GRAD_FLOATS] scratch (quadrant partials summed); with pair_grads */
-  int64_t num_slots;           /* T */
+  float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS] scratch (g's partials summed); with pair_grads */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
 

@@ -92,8 +92,7 @@ class GsProjectBwdArgs(C.Structure):
         ("rects", _vp), ("pair_offset", _vp), ("order", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
         ("g_conics", _vp), ("d_xyz", _vp), ("d_cov3d", _vp), ("d_scaling", _vp),
         ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
-        ("slot_live", _vp), ("slot_sums", _vp),
-        ("num_slots", C.c_int64),
+        ("slot_live", _vp), ("grad_sums", _vp),
     ]
 
 

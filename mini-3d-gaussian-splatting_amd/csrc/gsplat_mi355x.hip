@@ -821,7 +821,8 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
 //    pixel into a group buffer: dop = dL/d opacity and the contribution
 //    weight c, whose sign bit flags exp(-s/2) > 1 (the weight clamp then
 //    blocks dL/ds).
-//  B (entry-parallel), once per kBwdGroup live entries: lanes 8j..8j+7 sum
+//  B (entry-parallel), per chunk of up to kBwdGroup live entries of a
+//    64-entry word (records still staged): lanes 8j..8j+7 sum
 //    entry j's 64 pixels -- lane 8j + x takes column x, rows 0..7 -- into the
 //    10 gradient values and reduce them with 3 DPP steps.
 // The records of a 64-entry word's live entries are gathered lane-parallel
@@ -867,7 +868,7 @@ __device__ __forceinline__ void quad_tile(int &tile, int &quad) {
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
-  __shared__ float4 s_gi[kBwdGroup][2];  // group entry: (mx, my, q00, qo), (q11, -o/2, slot bits, 0)
+  __shared__ int s_idx[kBwdGroup];       // chunk entry j's bit in the word
   __shared__ float2 s_wrec[kWave * 6];   // the word's live records; word 10 = the entry's slot
   int tile, quad;
   quad_tile(tile, quad);
@@ -942,16 +943,22 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       r2 = recs[3 * (size_t)gid + 2];
     }
   };
-  int k = 0;             // entries in the group buffer (wave-uniform)
-  uint32_t gsimple = 0;  // bit j: group entry j is simple_entry, so phase B needs no clamp mask
-  auto phase_b = [&](auto masked_tag) {
+  // Phase B over a chunk: the k live entries of the current word whose bits
+  // cm holds (bit order = group order); their records are still staged.
+  auto phase_b = [&](auto masked_tag, unsigned long long cm, int k) {
     constexpr bool kMasked = decltype(masked_tag)::value;
-    // this wave's group writes have landed before other lanes read them
+    // each chunk entry's lane publishes its bit at the entry's rank in cm
+    if ((cm >> lane) & 1ull)
+      s_idx[__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u))] = lane;
+    // this wave's LDS writes have landed before other lanes read them
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int j = lane >> 3, col = lane & 7;
     if (j < k) {
-      const float4 ia = s_gi[j][0], ib = s_gi[j][1];
-      const float hop = ib.y;
+      const int bit = s_idx[j];
+      const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * bit];  // mx my q00 qo
+      const float2 ib = s_wrec[6 * bit + 2];                                // q11 o
+      const uint32_t slot = __float_as_uint(s_wrec[6 * bit + 5].x);
+      const float hop = -0.5f * ib.y;
       // this lane's pixels (x0 + col, y0 + r), r = 0..7: dx = bx, dy = by + r
       const float bx = (float)(x0 + col) - ia.x, by = (float)y0 - ia.y;
       float S0 = 0.f, Soy = 0.f, Soyy = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
@@ -986,7 +993,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float q00 = ia.z, qo = ia.w, q11 = ib.x;
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
-        const size_t e = (size_t)__float_as_uint(ib.z) * 4u + (uint32_t)quad;
+        const size_t e = (size_t)slot * 4u + (uint32_t)quad;
         float2 *out = reinterpret_cast<float2 *>(a.pair_grads + e * GS_PAIR_GRAD_FLOATS);
         out[0] = make_float2(g0, g1);
         out[1] = make_float2(g2, g3);
@@ -996,8 +1003,6 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         a.slot_live[e] = 1;
       }
     }
-    k = 0;
-    gsimple = 0;
   };
   unsigned long long mcur = live_word(0);
   fetch(0, mcur);
@@ -1020,8 +1025,13 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
     unsigned long long m = mcur;
     while (m) {
+     // a chunk: the word's next (up to) kBwdGroup live entries
+     unsigned long long cm = 0;
+     int k = 0;
+     do {
       const uint32_t bit = (uint32_t)__builtin_ctzll(m);
       m &= m - 1ull;
+      cm |= 1ull << bit;
       const uint32_t i = 64u * wd + bit;
       // two b128 broadcasts and a b64: (mx my q00 qo) (q11 o r g) (b z)
       const float4 r0v = reinterpret_cast<const float4 *>(s_wrec)[3 * bit];
@@ -1076,54 +1086,68 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         cw = (w == e) ? c : -c;  // c == +0 when skipped
       }
       s_dc[k][lane] = make_float2(dop, cw);
-      if (lane == 0) {
-        const float2 ps = s_wrec[6 * bit + 5];
-        s_gi[k][0] = make_float4(pm.x, pm.y, pq.x, pq.y);
-        s_gi[k][1] = make_float4(po.x, -0.5f * po.y, ps.x, 0.f);
-      }
-      gsimple |= (uint32_t)simple << k;
-      if (++k == kBwdGroup) {
-        if (gsimple == (1u << kBwdGroup) - 1u) phase_b(std::false_type{}); else phase_b(std::true_type{});
-      }
+      ++k;
+     } while (m && k < kBwdGroup);
+     if ((simple_w & cm) == cm) phase_b(std::false_type{}, cm, k); else phase_b(std::true_type{}, cm, k);
     }
     mcur = mnext;
-  }
-  if (k) {
-    if (gsimple == (1u << k) - 1u) phase_b(std::false_type{}); else phase_b(std::true_type{});
   }
 }
 
 // ======================================================== project bwd =====
-// Sum of each slot's quadrant partials: 4 lanes per slot (lane q reads
-// quadrant q's partial where slot_live flags it), added in a fixed DPP order
-// -- bitwise reproducible.  Slot-major, so a wave's loads cover one
-// contiguous run of slots (coalesced); the slot sums are then read by
-// k_project_bwd per Gaussian, whose slots are consecutive.
+// Sum of each Gaussian's gradient partials: 4 lanes per Gaussian, lane q
+// walks g's slots [pair_offset[g], pair_offset[g] + touches) and adds the
+// quadrant-q partials slot_live flags (slot order), then the 4 lane sums are
+// added in a fixed DPP order -- bitwise reproducible.  The four lanes of a
+// slot read its 160-B partial record together, and consecutive Gaussians'
+// slots are adjacent (index-order slots): coalesced.  Flags of 4 slots are
+// loaded at once, then their partials: two round trips per 4 slots.
 __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) {
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const long long e = t >> 2;
-  const int q = (int)(t & 3);
+  const int g = (int)(t >> 2), q = (int)(t & 3);
   constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
-  float2 v[kF2];
+  float2 acc[kF2];
 #pragma unroll
-  for (int k = 0; k < kF2; ++k) v[k] = make_float2(0.f, 0.f);
-  if (e < a.num_slots && a.slot_live[t]) {
-    const float2 *src = reinterpret_cast<const float2 *>(a.pair_grads) + (size_t)t * kF2;
+  for (int k = 0; k < kF2; ++k) acc[k] = make_float2(0.f, 0.f);
+  if (g < a.g.n && a.vis[g]) {
+    int tx0, tx1, ty0, ty1;
+    unpack_rect(a.rects, (uint32_t)g, tx0, tx1, ty0, ty1);
+    const uint32_t cnt = rect_touches(tx0, tx1, ty0, ty1);
+    const size_t off = a.pair_offset[g];
+    const uint8_t *flag = a.slot_live + off * 4 + q;  // (slot e, q) at flag[4 e]
+    const float2 *part = reinterpret_cast<const float2 *>(a.pair_grads) + (off * 4 + q) * kF2;  // at part[e * 4 kF2]
+    for (uint32_t e0 = 0; e0 < cnt; e0 += 4) {
+      uint32_t f[4];
 #pragma unroll
-    for (int k = 0; k < kF2; ++k) v[k] = src[k];
+      for (int i = 0; i < 4; ++i) f[i] = e0 + i < cnt ? flag[4 * (e0 + i)] : 0u;
+      float2 v[4][kF2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < kF2; ++k) v[i][k] = f[i] ? part[(size_t)(e0 + i) * 4 * kF2 + k] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (!f[i]) continue;
+#pragma unroll
+        for (int k = 0; k < kF2; ++k) {
+          acc[k].x += v[i][k].x;
+          acc[k].y += v[i][k].y;
+        }
+      }
+    }
   }
-  // (p0 + p1) + (p2 + p3) on every lane of the quad
+  // (q0 + q1) + (q2 + q3) on every lane of the quad
 #pragma unroll
   for (int k = 0; k < kF2; ++k) {
-    v[k].x += dpp_row<0xB1>(v[k].x);
-    v[k].y += dpp_row<0xB1>(v[k].y);
-    v[k].x += dpp_row<0x4E>(v[k].x);
-    v[k].y += dpp_row<0x4E>(v[k].y);
+    acc[k].x += dpp_row<0xB1>(acc[k].x);
+    acc[k].y += dpp_row<0xB1>(acc[k].y);
+    acc[k].x += dpp_row<0x4E>(acc[k].x);
+    acc[k].y += dpp_row<0x4E>(acc[k].y);
   }
-  if (q == 0 && e < a.num_slots) {
-    float2 *out = reinterpret_cast<float2 *>(a.slot_sums) + (size_t)e * kF2;
+  if (q == 0 && g < a.g.n) {
+    float2 *out = reinterpret_cast<float2 *>(a.grad_sums) + (size_t)g * kF2;
 #pragma unroll
-    for (int k = 0; k < kF2; ++k) out[k] = v[k];
+    for (int k = 0; k < kF2; ++k) out[k] = acc[k];
   }
 }
 
@@ -1135,39 +1159,13 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   float acc[GS_PAIR_GRAD_FLOATS];
 #pragma unroll
   for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
-  if (a.vis[g] && a.pair_grads) {
-    int tx0, tx1, ty0, ty1;
-    unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
-    const uint32_t cnt = rect_touches(tx0, tx1, ty0, ty1);
-    const uint32_t off = a.pair_offset[g];
-    // g's slot sums (k_gather_slots) are consecutive, and so are those of
-    // g + 1 (index-order slots): coalesced across the wave
-    const float2 *sl = reinterpret_cast<const float2 *>(a.slot_sums + (size_t)off * GS_PAIR_GRAD_FLOATS);
-    constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
-    uint32_t e = 0;
-    // four slots' loads in flight per round trip (the summation order stays
-    // slot by slot)
-    for (; e + 4 <= cnt; e += 4) {
-      float2 v[4][kF2];
+  if (a.pair_grads) {  // g's partials summed (k_gather_slots)
+    const float2 *gs = reinterpret_cast<const float2 *>(a.grad_sums) + (size_t)g * (GS_PAIR_GRAD_FLOATS / 2);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int k = 0; k < kF2; ++k) v[i][k] = sl[(e + i) * kF2 + k];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int k = 0; k < kF2; ++k) {
-          acc[2 * k] += v[i][k].x;
-          acc[2 * k + 1] += v[i][k].y;
-        }
-    }
-    for (; e < cnt; ++e) {
-#pragma unroll
-      for (int k = 0; k < kF2; ++k) {
-        const float2 v = sl[e * kF2 + k];
-        acc[2 * k] += v.x;
-        acc[2 * k + 1] += v.y;
-      }
+    for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) {
+      const float2 v = gs[k];
+      acc[2 * k] = v.x;
+      acc[2 * k + 1] = v.y;
     }
   }
   double dm0 = acc[0], dm1 = acc[1];
@@ -1568,13 +1566,13 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   if (!a->g.xyz || !a->g.color_logits || !a->means2d || !a->conics || !a->vis || !a->rects ||
       !a->pair_offset || !a->d_xyz || !a->d_color_logits || !a->d_opacity ||
       (raw ? (!a->g.scaling || !a->g.rotation || !a->d_scaling || !a->d_rotation) : !a->d_cov3d) ||
-      (a->pair_grads && (!a->slot_live || !a->slot_sums || a->num_slots < 0)))
+      (a->pair_grads && (!a->slot_live || !a->grad_sums)))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_project_backward");
   if (a->g.sh_degree < 0 || a->g.sh_degree > 3 || (a->g.sh_degree > 0 && (!a->g.sh_rest || !a->d_sh_rest)))
     return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest and d_sh_rest when > 0",
                 "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
-  if (a->pair_grads && a->num_slots > 0) k_gather_slots<<<div_up(4LL * a->num_slots, kBlock), kBlock, 0, s>>>(*a);
+  if (a->pair_grads) k_gather_slots<<<div_up(4LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
   k_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_backward");
 }

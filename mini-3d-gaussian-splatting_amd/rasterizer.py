@@ -314,14 +314,13 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     gc = None if g_conics is None else g_conics.contiguous()
     d_sh = buf("sh_rest", (n, N.GS_SH_REST, 3)) if sh_degree > 0 else None
     gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
-    slot_sums = None if pair_grads is None else torch.empty((fr.T, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
+    grad_sums = None if pair_grads is None else torch.empty((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
     pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
                             # Gaussian order (order=NULL): inputs/outputs stream; walking in depth
                             # order coalesces the slot reads but scatters 10 arrays (measured 2.4x slower)
                             N.ptr(fr.pair_offset), None, N.ptr(pair_grads), N.ptr(gm), N.ptr(gc), N.ptr(d_xyz),
                             N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op), N.ptr(d_sh),
-                            N.ptr(slot_live), N.ptr(slot_sums),
-                            fr.T if pair_grads is not None else 0)
+                            N.ptr(slot_live), N.ptr(grad_sums))
     StageTimer.mark("project_bwd")
     N.check(lib.gs_project_backward(C.byref(pb), s), "gs_project_backward")
     StageTimer.mark("~end_bwd")
