@@ -1095,16 +1095,17 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
 }
 
 // ======================================================== project bwd =====
-// Sum of each Gaussian's gradient partials: 4 lanes per Gaussian, lane q
-// walks g's slots [pair_offset[g], pair_offset[g] + touches) and adds the
-// quadrant-q partials slot_live flags (slot order), then the 4 lane sums are
-// added in a fixed DPP order -- bitwise reproducible.  The four lanes of a
-// slot read its 160-B partial record together, and consecutive Gaussians'
-// slots are adjacent (index-order slots): coalesced.  Flags of 4 slots are
-// loaded at once, then their partials: two round trips per 4 slots.
+// Sum of each Gaussian's gradient partials: 8 lanes per Gaussian, lane
+// (h, q) walks g's slots h, h+2, h+4, ... of [pair_offset[g], pair_offset[g]
+// + touches) and adds the quadrant-q partials slot_live flags (slot order),
+// then the 8 lane sums are added in a fixed DPP order -- bitwise
+// reproducible.  The four q lanes of a slot read its 160-B partial record
+// together, and consecutive Gaussians' slots are adjacent (index-order
+// slots): coalesced.  Flags of up to 4 slots are loaded at once, then their
+// partials: two round trips per 8 slots of g (the mean is 4.4 on C3).
 __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) {
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const int g = (int)(t >> 2), q = (int)(t & 3);
+  const int g = (int)(t >> 3), h = (int)((t >> 2) & 1), q = (int)(t & 3);
   constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
   float2 acc[kF2];
 #pragma unroll
@@ -1116,15 +1117,16 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
     const size_t off = a.pair_offset[g];
     const uint8_t *flag = a.slot_live + off * 4 + q;  // (slot e, q) at flag[4 e]
     const float2 *part = reinterpret_cast<const float2 *>(a.pair_grads) + (off * 4 + q) * kF2;  // at part[e * 4 kF2]
-    for (uint32_t e0 = 0; e0 < cnt; e0 += 4) {
+    for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += 8) {
       uint32_t f[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) f[i] = e0 + i < cnt ? flag[4 * (e0 + i)] : 0u;
+      for (int i = 0; i < 4; ++i) f[i] = e0 + 2 * i < cnt ? flag[4 * (e0 + 2 * i)] : 0u;
       float2 v[4][kF2];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int k = 0; k < kF2; ++k) v[i][k] = f[i] ? part[(size_t)(e0 + i) * 4 * kF2 + k] : make_float2(0.f, 0.f);
+        for (int k = 0; k < kF2; ++k)
+          v[i][k] = f[i] ? part[(size_t)(e0 + 2 * i) * 4 * kF2 + k] : make_float2(0.f, 0.f);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (!f[i]) continue;
@@ -1136,15 +1138,13 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
       }
     }
   }
-  // (q0 + q1) + (q2 + q3) on every lane of the quad
+  // ((q0 + q1) + (q2 + q3)) + (the other slot half's), on every lane of the 8
 #pragma unroll
   for (int k = 0; k < kF2; ++k) {
-    acc[k].x += dpp_row<0xB1>(acc[k].x);
-    acc[k].y += dpp_row<0xB1>(acc[k].y);
-    acc[k].x += dpp_row<0x4E>(acc[k].x);
-    acc[k].y += dpp_row<0x4E>(acc[k].y);
+    acc[k].x = oct_sum(acc[k].x);
+    acc[k].y = oct_sum(acc[k].y);
   }
-  if (q == 0 && g < a.g.n) {
+  if ((t & 7) == 0 && g < a.g.n) {
     float2 *out = reinterpret_cast<float2 *>(a.grad_sums) + (size_t)g * kF2;
 #pragma unroll
     for (int k = 0; k < kF2; ++k) out[k] = acc[k];
@@ -1572,7 +1572,7 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
     return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest and d_sh_rest when > 0",
                 "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
-  if (a->pair_grads) k_gather_slots<<<div_up(4LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  if (a->pair_grads) k_gather_slots<<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
   k_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_backward");
 }
