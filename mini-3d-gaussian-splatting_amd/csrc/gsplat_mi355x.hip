@@ -355,10 +355,11 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
       float op = a.g.opacity[(int64_t)g * a.g.opacity_stride];
       if (a.g.opacity_is_logit) op = 1.f / (1.f + expf(-op));  // get_opacity
       float4 *rec = reinterpret_cast<float4 *>(a.records) + 3 * (int64_t)g;
-      // record: mx my q00 qo | q11 o r g | b z off rinfo  (read as 8-byte pairs by the blend)
+      // record: mx my q00 q11 | qo o r g | b z off rinfo -- (q00, q11) adjacent so
+      // that the blend's dx^2 q00, dy^2 q11 are one packed multiply
       const float cr = 1.f / (1.f + expf(-cl[0])), cg = 1.f / (1.f + expf(-cl[1])), cb = 1.f / (1.f + expf(-cl[2]));  // sigmoid (:90)
-      rec[0] = make_float4(mx, my, q0, q1 + q2);
-      rec[1] = make_float4(q3, op, cr, cg);
+      rec[0] = make_float4(mx, my, q0, q3);
+      rec[1] = make_float4(q1 + q2, op, cr, cg);
       rec[2] = make_float4(cb, Z, 0.f, __uint_as_float(rinfo));
     }
     reinterpret_cast<uint2 *>(a.rects)[g] = make_uint2(rx, ry);
@@ -720,7 +721,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
       d[0] = n0;
       d[1] = n1;
       d[2] = n2;
-      const uint32_t qm = (b + threadIdx.x < end) ? quad_mask(n0.x, n0.y, n0.z, n0.w, n1.x, tx0, ty0) : 0u;
+      const uint32_t qm = (b + threadIdx.x < end) ? quad_mask(n0.x, n0.y, n0.z, n1.x, n0.w, tx0, ty0) : 0u;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const unsigned long long bq = __builtin_amdgcn_ballot_w64((qm >> q) & 1u);
@@ -753,9 +754,10 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         const uint32_t bit = (uint32_t)__builtin_ctzll(m);
         m &= ~(1ull << bit);
         const uint32_t j = 64u * wd + bit;
+        // pq = (q00, q11), po = (qo, opacity)
         const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
         const float dx = fx - pm.x, dy = fy - pm.y;
-        const float s = conic_s(dx, dy, pq.x, pq.y, po.x);  // :333
+        const float s = conic_s(dx, dy, pq.x, po.x, pq.y);  // :333
         // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp
         const bool run = A < kAlphaStop;  // the pixel has not terminated
         const bool live = run && !(s > 23.1f);
@@ -827,15 +829,29 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
 //    10 gradient values and reduce them with 3 DPP steps.
 // The records of a 64-entry word's live entries are gathered lane-parallel
 // one word ahead (registers), staged in LDS and read back as broadcasts.
-constexpr int kBwdGroup = 8;  // live entries per phase-B group
+#ifndef GS_BWD_GROUP
+#define GS_BWD_GROUP 8
+#endif
+constexpr int kBwdGroup = GS_BWD_GROUP;  // live entries per phase-B group: 8 or 4
+static_assert(kBwdGroup == 8 || kBwdGroup == 4, "phase B maps 8 or 16 lanes to an entry");
+constexpr int kBwdLanes = kWave / kBwdGroup;  // lanes per entry in phase B (8 or 16)
+constexpr int kBwdStep = kBwdLanes / 8;       // row step of a lane's pixels (1 or 2)
 // Group buffer rows (dop, c) are padded to 72 float2: phase B's lanes 8j + x
 // read row j at pixel x + 8r, and 72 puts rows j = 0..3 of a 32-lane half on
 // distinct banks (a stride of 64 would be a 4-way conflict).
-constexpr int kBwdRow = kWave + 8;
+constexpr int kBwdRow = kBwdGroup == 8 ? kWave + 8 : kWave + 16;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// Sum over the 16 lanes of each DPP row; every lane of the row gets the sum.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_row<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_row<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_row<0x124>(v);  // row_ror:4
+  v += dpp_row<0x128>(v);  // row_ror:8
+  return v;
 }
 // Sum over the 8 lanes 8j..8j+7 (a DPP half row); each of them gets the sum.
 __device__ __forceinline__ float oct_sum(float v) {
@@ -850,7 +866,7 @@ __device__ __forceinline__ float oct_sum(float v) {
 // at every pixel).  Then exp(-s/2) <= 1 and o w <= 1, and an accepted pair
 // has c = (1 - A) o w >= 0.005 * 1e-20 * 1e-5 > 0.
 __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
-  const float q00 = r0.z, qo = r0.w, q11 = r1.x, o = r1.y;
+  const float q00 = r0.z, q11 = r0.w, qo = r1.x, o = r1.y;
   const float q01 = 0.5f * qo;
   const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
   return o >= 1e-20f && o <= 1.f && tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det;
@@ -952,19 +968,19 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       s_idx[__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u))] = lane;
     // this wave's LDS writes have landed before other lanes read them
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int j = lane >> 3, col = lane & 7;
+    const int j = lane / kBwdLanes, sub = lane % kBwdLanes, col = sub & 7, row0 = sub >> 3;
     if (j < k) {
       const int bit = s_idx[j];
-      const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * bit];  // mx my q00 qo
-      const float2 ib = s_wrec[6 * bit + 2];                                // q11 o
+      const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * bit];  // mx my q00 q11
+      const float2 ib = s_wrec[6 * bit + 2];                                // qo o
       const uint32_t slot = __float_as_uint(s_wrec[6 * bit + 5].x);
       const float hop = -0.5f * ib.y;
       // this lane's pixels (x0 + col, y0 + r), r = 0..7: dx = bx, dy = by + r
-      const float bx = (float)(x0 + col) - ia.x, by = (float)y0 - ia.y;
+      const float bx = (float)(x0 + col) - ia.x, by = (float)(y0 + row0) - ia.y;
       float S0 = 0.f, Soy = 0.f, Soyy = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int p = col + 8 * r;  // phase A's lane of that pixel
+      for (int r = 0; r < kBwdGroup; ++r) {
+        const int p = col + 8 * (row0 + kBwdStep * r);  // phase A's lane of that pixel
         const float2 dc = s_dc[j][p];
         const float dop = dc.x, cs = dc.y;
         const float4 pg = s_pg[p];
@@ -974,8 +990,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float cw = fabsf(cs);
         S0 += ds;
         if (r) {
-          Soy = __builtin_fmaf(ds, (float)r, Soy);
-          Soyy = __builtin_fmaf(ds, (float)(r * r), Soyy);
+          Soy = __builtin_fmaf(ds, (float)(kBwdStep * r), Soy);
+          Soyy = __builtin_fmaf(ds, (float)(kBwdStep * kBwdStep * r * r), Soyy);
         }
         g5 += dop;
         g6 = __builtin_fmaf(pg.x, cw, g6);
@@ -987,10 +1003,11 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       float Sx = bx * S0, Sy = __builtin_fmaf(by, S0, Soy);
       float g2 = bx * Sx, g3 = bx * Sy;
       float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
-      Sx = oct_sum(Sx); Sy = oct_sum(Sy); g2 = oct_sum(g2); g3 = oct_sum(g3); g4 = oct_sum(g4);
-      g5 = oct_sum(g5); g6 = oct_sum(g6); g7 = oct_sum(g7); g8 = oct_sum(g8); g9 = oct_sum(g9);
-      if (col == 0) {
-        const float q00 = ia.z, qo = ia.w, q11 = ib.x;
+      auto red = [](float v) { return kBwdLanes == 8 ? oct_sum(v) : row16_sum(v); };
+      Sx = red(Sx); Sy = red(Sy); g2 = red(g2); g3 = red(g3); g4 = red(g4);
+      g5 = red(g5); g6 = red(g6); g7 = red(g7); g8 = red(g8); g9 = red(g9);
+      if (sub == 0) {
+        const float q00 = ia.z, qo = ib.x, q11 = ia.w;
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
         const size_t e = (size_t)slot * 4u + (uint32_t)quad;
@@ -1028,19 +1045,23 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
      // a chunk: the word's next (up to) kBwdGroup live entries
      unsigned long long cm = 0;
      int k = 0;
-     do {
+     // unrolled: the group row k is a compile-time LDS offset
+#pragma unroll
+     for (int kk = 0; kk < kBwdGroup; ++kk) {
+      if (kk > 0 && !m) break;
       const uint32_t bit = (uint32_t)__builtin_ctzll(m);
       m &= m - 1ull;
       cm |= 1ull << bit;
       const uint32_t i = 64u * wd + bit;
-      // two b128 broadcasts and a b64: (mx my q00 qo) (q11 o r g) (b z)
+      // two b128 broadcasts and a b64: (mx my q00 q11) (qo o r g) (b z);
+      // pq = (q00, q11), po = (qo, opacity)
       const float4 r0v = reinterpret_cast<const float4 *>(s_wrec)[3 * bit];
       const float4 r1v = reinterpret_cast<const float4 *>(s_wrec)[3 * bit + 1];
       const float2 pbz = s_wrec[6 * bit + 4];
       const float2 pm = make_float2(r0v.x, r0v.y), pq = make_float2(r0v.z, r0v.w);
       const float2 po = make_float2(r1v.x, r1v.y), prg = make_float2(r1v.z, r1v.w);
       const float dx = fx - pm.x, dy = fy - pm.y;
-      const float sq = conic_s(dx, dy, pq.x, pq.y, po.x);
+      const float sq = conic_s(dx, dy, pq.x, po.x, pq.y);
       // exp(-11.55) < 1e-5: exact early skip (NaN falls through), as in the forward
       const bool live = (i < neval) && !(sq > 23.1f);
       const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
@@ -1085,9 +1106,9 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         dop = (c > 0.f) ? g : 0.f;
         cw = (w == e) ? c : -c;  // c == +0 when skipped
       }
-      s_dc[k][lane] = make_float2(dop, cw);
-      ++k;
-     } while (m && k < kBwdGroup);
+      s_dc[kk][lane] = make_float2(dop, cw);
+      k = kk + 1;
+     }
      if ((simple_w & cm) == cm) phase_b(std::false_type{}, cm, k); else phase_b(std::true_type{}, cm, k);
     }
     mcur = mnext;

@@ -71,7 +71,7 @@ def main():
             rec = fr.records[gid]  # [n,12]
             n = rec.shape[0]
             tx, ty = t % tx_n, t // tx_n
-            mx, my, q00, qo, q11 = rec[:, 0:1], rec[:, 1:2], rec[:, 2:3], rec[:, 3:4], rec[:, 4:5]
+            mx, my, q00, q11, qo = rec[:, 0:1], rec[:, 1:2], rec[:, 2:3], rec[:, 3:4], rec[:, 4:5]
             det = q00 * q11 - 0.25 * qo * qo
             sxx, syy = q11 / det, q00 / det
             hx, hy = torch.sqrt(L * sxx), torch.sqrt(L * syy)
