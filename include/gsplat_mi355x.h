@@ -36,6 +36,7 @@ extern "C" {
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_MAX_RECT_TILES 8   /* r <= 50 px -> an AABB spans at most 8 tiles per axis */
 #define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian, 8x8 quadrant) gradient partial */
+#define GS_PARTIAL_STRIDE 12   /* floats between partials in pair_grads (10 used; 16-B aligned) */
 #define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2..3] reserved */
 
 typedef enum gs_status {
@@ -224,7 +225,7 @@ typedef struct gs_blend_bwd_args {
   const float *g_depth;         /* [H,W] or NULL */
   const uint64_t *live_bits;    /* the forward's liveness bitmap */
   int64_t live_words;
-  float *pair_grads;            /* [T, 4, GS_PAIR_GRAD_FLOATS] */
+  float *pair_grads;            /* [T, 4, GS_PARTIAL_STRIDE] */
   uint8_t *slot_live;           /* [T, 4], zeroed by the caller */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
@@ -247,7 +248,7 @@ typedef struct gs_project_bwd_args {
   const uint32_t *pair_offset;
   const uint32_t *order;       /* [n] permutation to walk the Gaussians in, or NULL: index order
                                   (slots are numbered in index order, so NULL reads them coalesced) */
-  const float *pair_grads;     /* [T,4,GS_PAIR_GRAD_FLOATS]; may be NULL when T == 0 */
+  const float *pair_grads;     /* [T,4,GS_PARTIAL_STRIDE]; may be NULL when T == 0 */
   const float *g_means2d;      /* [n,2] or NULL */
   const float *g_conics;       /* [n,4] or NULL */
   float *d_xyz;                /* [n,3] */

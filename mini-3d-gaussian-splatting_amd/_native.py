@@ -23,6 +23,7 @@ LIB_PATH = os.environ.get("GS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 GS_TILE = 16
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
+GS_PARTIAL_STRIDE = 12  # floats between quadrant partials in pair_grads
 GS_NUM_COUNTERS = 4
 GS_ABI_VERSION = 5
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)

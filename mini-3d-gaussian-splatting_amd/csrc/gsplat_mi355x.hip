@@ -1011,12 +1011,10 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
         const size_t e = (size_t)slot * 4u + (uint32_t)quad;
-        float2 *out = reinterpret_cast<float2 *>(a.pair_grads + e * GS_PAIR_GRAD_FLOATS);
-        out[0] = make_float2(g0, g1);
-        out[1] = make_float2(g2, g3);
-        out[2] = make_float2(g4, g5);
-        out[3] = make_float2(g6, g7);
-        out[4] = make_float2(g8, g9);
+        float4 *out = reinterpret_cast<float4 *>(a.pair_grads + e * GS_PARTIAL_STRIDE);
+        out[0] = make_float4(g0, g1, g2, g3);
+        out[1] = make_float4(g4, g5, g6, g7);
+        *reinterpret_cast<float2 *>(out + 2) = make_float2(g8, g9);
         a.slot_live[e] = 1;
       }
     }
@@ -1131,31 +1129,37 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
   float2 acc[kF2];
 #pragma unroll
   for (int k = 0; k < kF2; ++k) acc[k] = make_float2(0.f, 0.f);
-  if (g < a.g.n && a.vis[g]) {
-    int tx0, tx1, ty0, ty1;
-    unpack_rect(a.rects, (uint32_t)g, tx0, tx1, ty0, ty1);
+  // (vis, rect and first slot in one round trip: the culled have empty rects anyway)
+  const bool valid = g < a.g.n;
+  const bool vis = valid && a.vis[valid ? g : 0];
+  int tx0, tx1, ty0, ty1;
+  unpack_rect(a.rects, valid ? (uint32_t)g : 0u, tx0, tx1, ty0, ty1);
+  const size_t off = a.pair_offset[valid ? g : 0];
+  if (vis) {
     const uint32_t cnt = rect_touches(tx0, tx1, ty0, ty1);
-    const size_t off = a.pair_offset[g];
     const uint8_t *flag = a.slot_live + off * 4 + q;  // (slot e, q) at flag[4 e]
-    const float2 *part = reinterpret_cast<const float2 *>(a.pair_grads) + (off * 4 + q) * kF2;  // at part[e * 4 kF2]
+    // quadrant-q partial of slot e at part[e * 4 * kS4] (48-B records: 16-B loads)
+    const float4 *part = reinterpret_cast<const float4 *>(a.pair_grads + (off * 4 + q) * GS_PARTIAL_STRIDE);
+    constexpr int kS4 = GS_PARTIAL_STRIDE / 4;
     for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += 8) {
       uint32_t f[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) f[i] = e0 + 2 * i < cnt ? flag[4 * (e0 + 2 * i)] : 0u;
-      float2 v[4][kF2];
+      float4 va[4], vb[4];
+      float2 vc[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int k = 0; k < kF2; ++k)
-          v[i][k] = f[i] ? part[(size_t)(e0 + 2 * i) * 4 * kF2 + k] : make_float2(0.f, 0.f);
+      for (int i = 0; i < 4; ++i) {
+        const float4 *src = part + (size_t)(e0 + 2 * i) * 4 * kS4;
+        va[i] = f[i] ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+        vb[i] = f[i] ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+        vc[i] = f[i] ? *reinterpret_cast<const float2 *>(src + 2) : make_float2(0.f, 0.f);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (!f[i]) continue;
-#pragma unroll
-        for (int k = 0; k < kF2; ++k) {
-          acc[k].x += v[i][k].x;
-          acc[k].y += v[i][k].y;
-        }
+        acc[0].x += va[i].x; acc[0].y += va[i].y; acc[1].x += va[i].z; acc[1].y += va[i].w;
+        acc[2].x += vb[i].x; acc[2].y += vb[i].y; acc[3].x += vb[i].z; acc[3].y += vb[i].w;
+        acc[4].x += vc[i].x; acc[4].y += vc[i].y;
       }
     }
   }

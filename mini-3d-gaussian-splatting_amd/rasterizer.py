@@ -290,7 +290,7 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_depth = None if g_depth is None else g_depth.contiguous()
         # one partial per (slot, 8x8 quadrant); only the quadrants that replay
         # an entry write theirs and set its flag
-        pair_grads = torch.empty((fr.T * 4, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
+        pair_grads = torch.empty((fr.T * 4, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
         slot_live = torch.zeros((fr.T * 4,), dtype=torch.uint8, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
