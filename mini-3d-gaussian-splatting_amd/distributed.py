@@ -34,6 +34,7 @@ class GradAllReduce:
         self.params: List[torch.nn.Parameter] = list(params)
         self._flat: Optional[torch.Tensor] = None
         self._sizes: List[int] = []
+        self._avg: Optional[bool] = None  # ReduceOp.AVG usable (nccl = RCCL); decided on first use
 
     def _bucket(self) -> torch.Tensor:
         sizes = [p.numel() for p in self.params]
@@ -79,12 +80,20 @@ class GradAllReduce:
             else:
                 v.copy_(p.grad.reshape(-1))
         world = self.dist.get_world_size(self.group)
-        if self.dist.get_backend(self.group) == "nccl":
+        if self._avg is None:
+            self._avg = self.dist.get_backend(self.group) == "nccl" and hasattr(self.dist.ReduceOp, "AVG")
+        if self._avg:
             # RCCL divides inside the reduction: no extra pass over the bucket
-            self.dist.all_reduce(flat, op=self.dist.ReduceOp.AVG, group=self.group)
-        else:
-            self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
-            flat.div_(world)
+            try:
+                self.dist.all_reduce(flat, op=self.dist.ReduceOp.AVG, group=self.group)
+                return self._copy_out(views, in_place)
+            except (RuntimeError, ValueError):
+                self._avg = False  # a build without AVG: sum, then divide (the bucket is unchanged)
+        self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
+        flat.div_(world)
+        self._copy_out(views, in_place)
+
+    def _copy_out(self, views, in_place) -> None:
         for p, v, ok in zip(self.params, views, in_place):
             if ok:
                 continue
