@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI) for the driver; gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="init the process group and all-reduce even at world size 1 (rehearses the RCCL path)")
     return ap.parse_args()
 
 
@@ -101,7 +103,7 @@ def main():
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))  # % only matters for a 1-GPU gloo rehearsal
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or a.force_dist:
         import torch.distributed as dist
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
