@@ -34,7 +34,10 @@ extern "C" {
 #define GS_ABI_VERSION 5
 #define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
-#define GS_MAX_RECT_TILES 8   /* r <= 50 px -> an AABB spans at most 8 tiles per axis */
+#define GS_MAX_RECT_TILES 8   /* an AABB spans at most 8 tiles per axis ...            */
+#define GS_MAX_RADIUS 55.0f   /* ... while radius_max <= 55 px (2*55+1 px wide); the
+                                 reference default is 50. gs_project_forward returns
+                                 GS_ERR_UNSUPPORTED for a larger radius_max. */
 #define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian, 8x8 quadrant) gradient partial */
 #define GS_PARTIAL_STRIDE 12   /* floats between partials in pair_grads (10 used; 16-B aligned) */
 #define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2..3] reserved */
@@ -59,7 +62,7 @@ typedef struct gs_camera {
   float fx, fy, cx, cy;
   float view[12];        /* row-major 3x4 [R | t] */
   float radius_min;      /* GaussianRenderer(radius_min=0.01) */
-  float radius_max;      /* GaussianRenderer(radius_max=50.0) */
+  float radius_max;      /* GaussianRenderer(radius_max=50.0); <= GS_MAX_RADIUS */
   float bg[3];           /* RenderSettings.bg_color */
   int32_t tile_size;     /* must be GS_TILE */
   float campos[3];       /* camera centre in world coordinates, -R^T t; read only when sh_degree > 0 */

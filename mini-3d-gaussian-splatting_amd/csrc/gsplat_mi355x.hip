@@ -557,13 +557,16 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
 }
 
 // Emission, coalesced: per round of 256 depth-ordered Gaussians, scan their
-// touch counts into LDS, then every thread writes consecutive output entries,
-// finding its Gaussian by binary search over the round's offsets.
+// touch counts into LDS and mark each output position with its Gaussian (a
+// byte per position: at most 256 x GS_MAX_RECT_TILES^2 = 16384 per round);
+// then every thread writes consecutive output entries, looking its Gaussian
+// up in one LDS read (a binary search over the offsets took 8 dependent ones).
 __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials) {
   __shared__ uint32_t s_off[kBlock + 1];
   __shared__ uint32_t s_g[kBlock];
   __shared__ uint2 s_rect[kBlock];
   __shared__ uint32_t s_tmp[4];
+  __shared__ uint8_t s_owner[kBlock * GS_MAX_RECT_TILES * GS_MAX_RECT_TILES];
   const long long base = (long long)blockIdx.x * kBinChunk;
   uint32_t out_base = partials[blockIdx.x];
   for (int r = 0; r < kBinChunk / kBlock; ++r) {
@@ -581,14 +584,10 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
     s_g[threadIdx.x] = g;
     s_rect[threadIdx.x] = rc;
     if (threadIdx.x == 0) s_off[kBlock] = tot;
+    for (uint32_t c = 0; c < cnt; ++c) s_owner[ex + c] = (uint8_t)threadIdx.x;
     __syncthreads();
     for (uint32_t o = threadIdx.x; o < tot; o += kBlock) {
-      // last i with s_off[i] <= o (entries with zero touches share offsets)
-      int lo = 0, hi = kBlock;  // invariant: s_off[lo] <= o < s_off[hi]
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (s_off[mid] <= o) lo = mid; else hi = mid;
-      }
+      const int lo = s_owner[o];
       const uint2 rr = s_rect[lo];
       const uint32_t tx0 = rr.x & 0xFFFFu, ty0 = rr.y & 0xFFFFu;
       const uint32_t wt = (rr.x >> 16) - tx0 + 1u;
@@ -1456,6 +1455,8 @@ const char *gs_last_error(void) { return g_err; }
 gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_project_forward");
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16 and image size positive", "gs_project_forward");
+  if (!(a->cam.radius_max <= GS_MAX_RADIUS))  // rects wider than GS_MAX_RECT_TILES (k_bin_emit's LDS map)
+    return fail(GS_ERR_UNSUPPORTED, "%s: radius_max must be <= GS_MAX_RADIUS (55 px)", "gs_project_forward");
   if (a->g.n < 0) return fail(GS_ERR_INVALID_ARG, "%s: bad n", "gs_project_forward");
   hipStream_t s = (hipStream_t)stream;
   if (a->g.n == 0) return GS_OK;

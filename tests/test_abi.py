@@ -64,6 +64,12 @@ def test_bad_arguments_are_reported(pkg):
     assert lib.gs_project_forward(C.byref(a), None) == 3  # unsupported tile size
     with pytest.raises(RuntimeError, match="gs_status=3"):
         N.check(lib.gs_project_forward(C.byref(a), None), "gs_project_forward")
+    a.cam.tile_size = 16
+    a.cam.radius_max = 56.0  # rects could span 9 tiles per axis (GS_MAX_RADIUS)
+    assert lib.gs_project_forward(C.byref(a), None) == 3
+    assert b"radius_max" in lib.gs_last_error()
+    a.cam.radius_max = float("nan")
+    assert lib.gs_project_forward(C.byref(a), None) == 3
 
 
 def test_loss_bad_arguments(pkg):
