@@ -1192,8 +1192,8 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
       acc[2 * k + 1] = v.y;
     }
   }
-  double dm0 = acc[0], dm1 = acc[1];
-  double G[4] = {acc[2], acc[3], acc[3], acc[4]};
+  float dm0 = acc[0], dm1 = acc[1];
+  float G[4] = {acc[2], acc[3], acc[3], acc[4]};
   if (a.g_means2d) {
     dm0 += a.g_means2d[2 * (size_t)g];
     dm1 += a.g_means2d[2 * (size_t)g + 1];
@@ -1215,7 +1215,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   }
   // SH: d rest_k = Y_k dlogit; the view direction's gradient reaches xyz
   // through dir = v / |v| (added to d_xyz below)
-  double dxyz_sh[3] = {0.0, 0.0, 0.0};
+  float dxyz_sh[3] = {0.f, 0.f, 0.f};
   if (a.g.sh_degree > 0) {
     const int nb = sh_rest_count(a.g.sh_degree);
     const float *r = a.g.sh_rest + (int64_t)g * a.g.sh_rest_stride;
@@ -1231,7 +1231,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
     }
     float dd[3];
     sh_basis_vjp(dir[0], dir[1], dir[2], wY, nb, dd);
-    const double dot = (double)dir[0] * dd[0] + (double)dir[1] * dd[1] + (double)dir[2] * dd[2];
+    const float dot = (dir[0] * dd[0] + dir[1] * dd[1]) + dir[2] * dd[2];
 #pragma unroll
     for (int j = 0; j < 3; ++j) dxyz_sh[j] = (dd[j] - dir[j] * dot) * inv_norm;
   }
@@ -1241,12 +1241,12 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
     dop = (dop * (1.f - o)) * o;
   }
   a.d_opacity[g] = dop;
-  const bool any = dm0 != 0.0 || dm1 != 0.0 || G[0] != 0.0 || G[1] != 0.0 || G[2] != 0.0 ||
-                   G[3] != 0.0 || acc[9] != 0.f;
+  const bool any = dm0 != 0.f || dm1 != 0.f || G[0] != 0.f || G[1] != 0.f || G[2] != 0.f ||
+                   G[3] != 0.f || acc[9] != 0.f;
   const bool raw = a.g.cov3d == nullptr;
   if (!any) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.d_xyz[3 * (size_t)g + k] = (float)dxyz_sh[k];
+    for (int k = 0; k < 3; ++k) a.d_xyz[3 * (size_t)g + k] = dxyz_sh[k];
     if (raw) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) a.d_scaling[3 * (size_t)g + k] = 0.f;
@@ -1258,8 +1258,16 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
     }
     return;
   }
+  // The screen-space part (conic inverse backward, dL/dJ, dL/dmean) runs in
+  // double: for needle Gaussians Q = inv(cov2d) has condition numbers ~1e6
+  // and dV = -Q G Q cancels against J C in dL/dJ.  The 3D part (J^T dV J,
+  // Rv^T dC Rv, scale/rotation) is plain fp32 with the triple products
+  // factored -- f64 exp/div/sqrt and 81-term sums made this kernel 3x slower.
   const gs_camera &c = a.cam;
-  const float *R = c.view;
+  const float *R = c.view;  // rows [R | t]
+  auto dot3 = [](float a0, float a1, float a2, float b0, float b1, float b2) {
+    return __builtin_fmaf(a0, b0, __builtin_fmaf(a1, b1, a2 * b2));
+  };
   float Sf[9];
   if (!raw) {
 #pragma unroll
@@ -1273,7 +1281,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
     Xc[i] = (double)X3[0] * R[i * 4] + (double)X3[1] * R[i * 4 + 1] + (double)X3[2] * R[i * 4 + 2] + R[i * 4 + 3];
   const double X = Xc[0], Y = Xc[1], Z = Xc[2];
   const double fx = c.fx, fy = c.fy;
-  double RS[9], C[9];
+  double RS[9], C[9];  // C = Rv Sigma Rv^T
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1284,54 +1292,29 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       C[i * 3 + j] = RS[i * 3] * R[j * 4] + RS[i * 3 + 1] * R[j * 4 + 1] + RS[i * 3 + 2] * R[j * 4 + 2];
-  const double iz = 1.0 / Z;
-  const double J[6] = {fx * iz, 0.0, -fx * X * iz * iz, 0.0, -fy * iz, fy * Y * iz * iz};
+  const double iz = 1.0 / Z, iz2 = iz * iz, iz3 = iz2 * iz;
+  const double Jd[6] = {fx * iz, 0.0, -fx * X * iz2, 0.0, -fy * iz, fy * Y * iz2};
   const float4 Qf = reinterpret_cast<const float4 *>(a.conics)[g];
   const double Q[4] = {Qf.x, Qf.y, Qf.z, Qf.w};
   // d cov2d = -Q^T G Q^T (inverse backward)
   const double QG0 = Q[0] * G[0] + Q[2] * G[2], QG1 = Q[0] * G[1] + Q[2] * G[3];
   const double QG2 = Q[1] * G[0] + Q[3] * G[2], QG3 = Q[1] * G[1] + Q[3] * G[3];
-  const double dV[4] = {-(QG0 * Q[0] + QG1 * Q[1]), -(QG0 * Q[2] + QG1 * Q[3]), -(QG2 * Q[0] + QG3 * Q[1]),
-                        -(QG2 * Q[2] + QG3 * Q[3])};
+  const double dVd[4] = {-(QG0 * Q[0] + QG1 * Q[1]), -(QG0 * Q[2] + QG1 * Q[3]), -(QG2 * Q[0] + QG3 * Q[1]),
+                         -(QG2 * Q[2] + QG3 * Q[3])};
   double JCt[6], JCn[6];  // J C^T, J C
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      JCt[i * 3 + j] = J[i * 3] * C[j * 3] + J[i * 3 + 1] * C[j * 3 + 1] + J[i * 3 + 2] * C[j * 3 + 2];
-      JCn[i * 3 + j] = J[i * 3] * C[j] + J[i * 3 + 1] * C[3 + j] + J[i * 3 + 2] * C[6 + j];
+      JCt[i * 3 + j] = Jd[i * 3] * C[j * 3] + Jd[i * 3 + 1] * C[j * 3 + 1] + Jd[i * 3 + 2] * C[j * 3 + 2];
+      JCn[i * 3 + j] = Jd[i * 3] * C[j] + Jd[i * 3 + 1] * C[3 + j] + Jd[i * 3 + 2] * C[6 + j];
     }
   double dJ[6];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      dJ[i * 3 + j] = dV[i * 2] * JCt[j] + dV[i * 2 + 1] * JCt[3 + j] + dV[i] * JCn[j] + dV[2 + i] * JCn[3 + j];
-  double dC[9];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      double v = 0.0;
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int l = 0; l < 2; ++l) v += J[k * 3 + i] * dV[k * 2 + l] * J[l * 3 + j];
-      dC[i * 3 + j] = v;
-    }
-  double dS[9];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      double v = 0.0;
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int l = 0; l < 3; ++l) v += (double)R[k * 4 + i] * dC[k * 3 + l] * R[l * 4 + j];
-      dS[i * 3 + j] = v;
-    }
-  const double iz2 = iz * iz, iz3 = iz2 * iz;
+      dJ[i * 3 + j] = dVd[i * 2] * JCt[j] + dVd[i * 2 + 1] * JCt[3 + j] + dVd[i] * JCn[j] + dVd[2 + i] * JCn[3 + j];
   const double dX = dm0 * fx * iz + dJ[2] * (-fx * iz2);
   const double dY = dm1 * (-fy * iz) + dJ[5] * (fy * iz2);
   const double dZ = dm0 * (-fx * X * iz2) + dm1 * (fy * Y * iz2) + dJ[0] * (-fx * iz2) +
@@ -1339,50 +1322,71 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
                     (double)acc[9];
 #pragma unroll
   for (int j = 0; j < 3; ++j)
-    a.d_xyz[3 * (size_t)g + j] = (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ + dxyz_sh[j]);
+    a.d_xyz[3 * (size_t)g + j] = (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ + (double)dxyz_sh[j]);
+  float J[6], dV[4];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) J[k] = (float)Jd[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dV[k] = (float)dVd[k];
+  float dVJ[6], dC[9];  // dC = J^T dV J
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dVJ[k * 3 + j] = __builtin_fmaf(dV[k * 2], J[j], dV[k * 2 + 1] * J[3 + j]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dC[i * 3 + j] = __builtin_fmaf(J[i], dVJ[j], J[3 + i] * dVJ[3 + j]);
+  float dCR[9], dS[9];  // dS = Rv^T dC Rv
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dCR[k * 3 + j] = dot3(dC[k * 3], dC[k * 3 + 1], dC[k * 3 + 2], R[j], R[4 + j], R[8 + j]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dS[i * 3 + j] = dot3(R[i], R[4 + i], R[8 + i], dCR[j], dCR[3 + j], dCR[6 + j]);
   if (!raw) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) a.d_cov3d[9 * (size_t)g + k] = (float)dS[k];
+    for (int k = 0; k < 9; ++k) a.d_cov3d[9 * (size_t)g + k] = dS[k];
     return;
   }
   // raw path: Sigma = M M^T, M = R(q) diag(s), s = exp(scaling), q = normalize(rotation)
   const float *sc = a.g.scaling + (int64_t)g * 3, *rq = a.g.rotation + (int64_t)g * 4;
-  double qn = sqrt((double)rq[0] * rq[0] + (double)rq[1] * rq[1] + (double)rq[2] * rq[2] + (double)rq[3] * rq[3]);
-  qn = qn < 1e-12 ? 1e-12 : qn;
-  const double w = rq[0] / qn, x = rq[1] / qn, y = rq[2] / qn, z = rq[3] / qn;
-  const double Rq[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
-                        2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
-                        2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
-  const double s[3] = {exp((double)sc[0]), exp((double)sc[1]), exp((double)sc[2])};
-  double dM[9];
+  float qn = sqrtf(dot3(rq[0], rq[1], rq[2], rq[0], rq[1], rq[2]) + rq[3] * rq[3]);
+  qn = qn < 1e-12f ? 1e-12f : qn;
+  const float iq = 1.f / qn;
+  const float w = rq[0] * iq, x = rq[1] * iq, y = rq[2] * iq, z = rq[3] * iq;
+  const float Rq[9] = {1.f - 2.f * (y * y + z * z), 2.f * (x * y - w * z), 2.f * (x * z + w * y),
+                       2.f * (x * y + w * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - w * x),
+                       2.f * (x * z - w * y), 2.f * (y * z + w * x), 1.f - 2.f * (x * x + y * y)};
+  const float s3[3] = {expf(sc[0]), expf(sc[1]), expf(sc[2])};
+  float Ss[9];  // dS + dS^T
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      double v = 0.0;
+    for (int k = 0; k < 3; ++k) Ss[i * 3 + k] = dS[i * 3 + k] + dS[k * 3 + i];
+  float dR[9];  // dL/dRq = (dS + dS^T) Rq diag(s)^2
 #pragma unroll
-      for (int k = 0; k < 3; ++k) v += (dS[i * 3 + k] + dS[k * 3 + i]) * Rq[k * 3 + j] * s[j];
-      dM[i * 3 + j] = v;
-    }
+  for (int i = 0; i < 3; ++i)
 #pragma unroll
-  for (int j = 0; j < 3; ++j)
-    a.d_scaling[3 * (size_t)g + j] =
-        (float)((dM[j] * Rq[j] + dM[3 + j] * Rq[3 + j] + dM[6 + j] * Rq[6 + j]) * s[j]);
-  double dR[9];
+    for (int j = 0; j < 3; ++j)
+      dR[i * 3 + j] = dot3(Ss[i * 3], Ss[i * 3 + 1], Ss[i * 3 + 2], Rq[j], Rq[3 + j], Rq[6 + j]) * (s3[j] * s3[j]);
 #pragma unroll
-  for (int i = 0; i < 9; ++i) dR[i] = dM[i] * s[i % 3];
-  const double dw = 2 * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
-  const double dx = 2 * (y * dR[1] + z * dR[2] + y * dR[3] - 2 * x * dR[4] - w * dR[5] + z * dR[6] + w * dR[7] -
-                         2 * x * dR[8]);
-  const double dy = 2 * (-2 * y * dR[0] + x * dR[1] + w * dR[2] + x * dR[3] + z * dR[5] - w * dR[6] + z * dR[7] -
-                         2 * y * dR[8]);
-  const double dz = 2 * (-2 * z * dR[0] - w * dR[1] + x * dR[2] + w * dR[3] - 2 * z * dR[4] + y * dR[5] +
-                         x * dR[6] + y * dR[7]);
-  const double dot = dw * w + dx * x + dy * y + dz * z;
-  a.d_rotation[4 * (size_t)g + 0] = (float)((dw - w * dot) / qn);
-  a.d_rotation[4 * (size_t)g + 1] = (float)((dx - x * dot) / qn);
-  a.d_rotation[4 * (size_t)g + 2] = (float)((dy - y * dot) / qn);
-  a.d_rotation[4 * (size_t)g + 3] = (float)((dz - z * dot) / qn);
+  for (int j = 0; j < 3; ++j)  // dL/ds_j s_j: (dR / s_j) . Rq column j, times s_j
+    a.d_scaling[3 * (size_t)g + j] = dot3(dR[j], dR[3 + j], dR[6 + j], Rq[j], Rq[3 + j], Rq[6 + j]);
+  const float dw = 2.f * ((-z * dR[1] + y * dR[2]) + (z * dR[3] - x * dR[5]) + (-y * dR[6] + x * dR[7]));
+  const float dx = 2.f * ((y * dR[1] + z * dR[2]) + (y * dR[3] - 2.f * x * dR[4]) + (-w * dR[5] + z * dR[6]) +
+                          (w * dR[7] - 2.f * x * dR[8]));
+  const float dy = 2.f * ((-2.f * y * dR[0] + x * dR[1]) + (w * dR[2] + x * dR[3]) + (z * dR[5] - w * dR[6]) +
+                          (z * dR[7] - 2.f * y * dR[8]));
+  const float dz = 2.f * ((-2.f * z * dR[0] - w * dR[1]) + (x * dR[2] + w * dR[3]) + (-2.f * z * dR[4] + y * dR[5]) +
+                          (x * dR[6] + y * dR[7]));
+  const float dot = __builtin_fmaf(dw, w, __builtin_fmaf(dx, x, __builtin_fmaf(dy, y, dz * z)));
+  a.d_rotation[4 * (size_t)g + 0] = (dw - w * dot) * iq;
+  a.d_rotation[4 * (size_t)g + 1] = (dx - x * dot) * iq;
+  a.d_rotation[4 * (size_t)g + 2] = (dy - y * dot) * iq;
+  a.d_rotation[4 * (size_t)g + 3] = (dz - z * dot) * iq;
 }
 
 // tile coordinates are packed in 12 bits (record word 11): images up to 65536 px a side
