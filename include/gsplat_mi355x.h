@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 5
+#define GS_ABI_VERSION 6
 #define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_MAX_RECT_TILES 8   /* an AABB spans at most 8 tiles per axis ...            */
@@ -160,6 +160,9 @@ typedef struct gs_bin_args {
   uint32_t *pair_gauss;  /* [T] */
   uint32_t *pair_offset; /* [n] indexed by Gaussian id: first gradient slot (both calls write it) */
   float *records;        /* [n, GS_RECORD_FLOATS]: word 10 <- pair_offset bits */
+  int64_t capacity;      /* entries tile_keys / pair_gauss hold.  gs_bin_emit does nothing
+                            when T = counters[1] > capacity, so it may be queued before T is
+                            read back (then emit again into buffers of >= T entries) */
 } gs_bin_args;
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream);
 gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream);

@@ -25,7 +25,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 12  # floats between quadrant partials in pair_grads
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 5
+GS_ABI_VERSION = 6
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -61,6 +61,7 @@ class GsBinArgs(C.Structure):
         ("n", C.c_int32), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("sorted_ids", _vp),
         ("rects", _vp), ("vis", _vp), ("counters", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
         ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp), ("records", _vp),
+        ("capacity", C.c_int64),
     ]
 
 

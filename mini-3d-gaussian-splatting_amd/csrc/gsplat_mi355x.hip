@@ -567,6 +567,9 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   __shared__ uint2 s_rect[kBlock];
   __shared__ uint32_t s_tmp[4];
   __shared__ uint8_t s_owner[kBlock * GS_MAX_RECT_TILES * GS_MAX_RECT_TILES];
+  // T entries do not fit: do nothing (the caller re-emits into T-sized
+  // buffers; the slot pass below is not idempotent, so it must run once)
+  if ((long long)a.counters[1] > a.capacity) return;
   const long long base = (long long)blockIdx.x * kBinChunk;
   uint32_t out_base = partials[blockIdx.x];
   for (int r = 0; r < kBinChunk / kBlock; ++r) {
@@ -1537,9 +1540,10 @@ gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
 gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_bin_emit");
   if (a->n <= 0) return GS_OK;
-  if (!a->sorted_ids || !a->rects || !a->workspace || !a->tile_keys || !a->pair_gauss || !a->pair_offset ||
-      !a->records)
+  if (!a->sorted_ids || !a->rects || !a->counters || !a->workspace || !a->tile_keys || !a->pair_gauss ||
+      !a->pair_offset || !a->records)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_bin_emit");
+  if (a->capacity < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative capacity", "gs_bin_emit");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
   k_bin_emit<<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace);

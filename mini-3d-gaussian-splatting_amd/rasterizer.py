@@ -142,6 +142,7 @@ class _Frame:
 
 
 _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess)
+_HOST_COUNTERS: dict = {}  # device -> pinned int32[2] for the (M, T) read-back
 
 
 def _alloc_tile_buffers(lib, cap: int, num_tiles: int, dev):
@@ -193,7 +194,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         bws = torch.empty((lib.gs_bin_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         pair_offset = torch.empty((n,), dtype=i32, device=dev)
         ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(vis),
-                         N.ptr(counters), N.ptr(bws), bws.numel(), 0, 0, N.ptr(pair_offset), N.ptr(records))
+                         N.ptr(counters), N.ptr(bws), bws.numel(), 0, 0, N.ptr(pair_offset), N.ptr(records), 0)
         StageTimer.mark("bin_count")
         N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
         # everything whose size does not depend on T is allocated before the
@@ -206,11 +207,27 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         pix_acc = torch.empty((H * W, 4), dtype=f32, device=dev)
         pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
         # the T-sized buffers too, at a capacity guessed from the last frame on
-        # this device (re-allocated after the sync if T exceeds it)
+        # this device, and the emission queued into them before the sync (it
+        # drops entries past the capacity): its kernel time hides the
+        # read-back's round trip.  T above the guess: re-allocate, re-emit.
         cap = _T_SEEN.get(dev, 0)
         big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, dev) if cap else None
+        # (M, T) read back through pinned memory, copied BEFORE the emission
+        # is queued, so the host wakes while the GPU still emits
+        host = _HOST_COUNTERS.get(dev)
+        if host is None:
+            host = _HOST_COUNTERS[dev] = torch.empty((2,), dtype=i32, pin_memory=True)
+        host.copy_(counters[:2], non_blocking=True)
+        ready = torch.cuda.Event()
+        ready.record()
+        if big_guess is not None:
+            gb, gcap = big_guess[0].data_ptr(), big_guess[1]
+            ba.tile_keys, ba.pair_gauss, ba.capacity = gb, gb + 8 * gcap, gcap
+            StageTimer.mark("bin_emit")
+            N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
         StageTimer.mark("~sync")
-        M, T = (int(v) for v in counters[:2].tolist())  # the one host sync
+        ready.synchronize()  # the one host sync
+        M, T = (int(v) for v in host.tolist())
         _T_SEEN[dev] = T
     else:
         M, T = 0, 0
@@ -229,7 +246,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     # arithmetic: between the host sync and the blend launch the GPU idles,
     # so this span does no torch work (views of the sorted ids and the bitmap
     # are made after the blend is queued).
-    big, cap_t = big_guess if big_guess is not None and big_guess[1] >= T else _alloc_tile_buffers(lib, T, num_tiles, dev)
+    emitted = big_guess is not None and big_guess[1] >= T
+    big, cap_t = big_guess if emitted else _alloc_tile_buffers(lib, T, num_tiles, dev)
     tws_bytes = int(lib.gs_radix_sort_workspace_bytes(T))
     live_words = int(lib.gs_blend_live_words(T, num_tiles))
     base = big.data_ptr()
@@ -238,9 +256,10 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     o_ws = (16 * cap_t + 255) // 256 * 256
     o_live = o_ws + (int(lib.gs_radix_sort_workspace_bytes(cap_t)) + 255) // 256 * 256
     p_ws, p_live = base + o_ws, base + o_live
-    ba.tile_keys, ba.pair_gauss = p_tk[0], p_tv[0]
-    StageTimer.mark("bin_emit")
-    N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
+    if not emitted:
+        ba.tile_keys, ba.pair_gauss, ba.capacity = p_tk[0], p_tv[0], cap_t
+        StageTimer.mark("bin_emit")
+        N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
 
     bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
     alt = C.c_int32(0)

@@ -250,6 +250,31 @@ def test_deterministic(pkg, cuda):
         assert torch.equal(a, b)
 
 
+def test_emit_capacity_guess(pkg, cuda):
+    """The tile emission is queued before T is read back, into buffers sized
+    from the previous frame's T: a guess too small (emit skipped, re-emitted
+    after the sync), none (first frame) and a good one give bit-identical
+    frames and gradients."""
+    RZ = pkg.rasterizer
+    syn = pkg.synthetic
+    sc = syn.make_scene(50000, 480, 270, seed=6, sigma_range=(0.002, 0.02))
+    res = []
+    for guess in (None, 16, "last"):
+        if guess is None:
+            RZ._T_SEEN.pop(cuda, None)
+        elif guess != "last":
+            RZ._T_SEEN[cuda] = guess
+        m = syn.to_model(sc, pkg.GaussianModel, cuda)
+        out = pkg.GaussianRenderer().render(Cam(480, 270, sc.fovx, sc.fovy), m,
+                                            pkg.RenderSettings(270, 480, torch.zeros(3)))
+        (out["image"].sum() + out["depth"].sum()).backward()
+        res.append((out["image"].clone(), out["depth"].clone(), m._xyz.grad.clone(), m._opacity.grad.clone()))
+        assert RZ._T_SEEN[cuda] > 16
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert torch.equal(a, b)
+
+
 def test_fused_adam_matches_torch_adam(pkg, cuda):
     """FusedAdam (one gs_adam_step launch) vs torch.optim.Adam, 5 groups as in
     the reference's GaussianOptimizer (optimizer.py:100-113), one param without grad."""
