@@ -75,6 +75,9 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) {
 // ldexp, since 2^ph stays a normal float here.  ~1 ulp, like expf; forward
 // and backward share it, so their decisions replay bit-identically (C3:
 // the same 9 knife-edge pixels vs the oracle as the full expf sequence).
+// Dropping the log2(e) low-part term saves a VALU per evaluated pair (-20 us
+// per C3 step) but is <= 3 ulp at x = -11.6: 12 knife-edge pixels and the
+// scaling gradient's error 5.4e-4 -> 1.2e-3 of scale.  Not taken.
 __device__ __forceinline__ float exp_inrange(float x) {
   const float ph = x * 0x1.715476p+0f;
   float pl = __builtin_fmaf(x, 0x1.715476p+0f, -ph);
@@ -936,7 +939,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   const float K = (gR0 * tr + gR1 * tg) + (gR2 * tbl + gD * Dt);
   const float G0 = __builtin_fmaf(gA, onemA, -K);
   float P = (gR0 * bg0 + gR1 * bg1) + gR2 * bg2;
-  float A = 0.f;
+  float A = 0.f, T1 = 1.f;  // T1 = 1 - A, carried: the next entry's transmittance is this one's rcp argument
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   const unsigned long long *lw =
       reinterpret_cast<const unsigned long long *>(a.live_bits) + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile;
@@ -1074,11 +1077,12 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         // the same values.  wv = 0 exactly where the pair is skipped.
         const float w = exp_neg_half(sq);
         const float wv = (live && !(w < kMinWeight)) ? w : 0.f;
-        const float trans = 1.f - A;
+        const float trans = T1;
         const float c = trans * (po.y * wv);
         A = A + c;
         P = __builtin_fmaf(c, X, P);
-        const float inv = __builtin_amdgcn_rcpf(1.f - A);  // v_rcp_f32 (1 ulp): a gradient factor, no decision
+        T1 = 1.f - A;
+        const float inv = __builtin_amdgcn_rcpf(T1);  // v_rcp_f32 (1 ulp): a gradient factor, no decision
         const float d_live = __builtin_fmaf(inv, P + G0, X);
         // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
         const float dal = trans * (A >= kAlphaStop ? X + gA : d_live);
@@ -1089,15 +1093,16 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float w = sat01(e);
         const float u = po.y * w;
         const float ai = sat01(u);
-        const float trans = 1.f - A;
+        const float trans = T1;
         // the forward's skips folded into the weight exactly as there: c is
         // +0 for a skipped pair and > 0 for an accepted one (take <=> c > 0)
         const float c = trans * ((live && !(w < kMinWeight)) ? ai : 0.f);
         A = A + c;
         P = __builtin_fmaf(c, X, P);
         const bool term = A >= kAlphaStop;
+        T1 = 1.f - A;
         // both arms computed, then a select: no divergent branch per entry
-        const float inv = __builtin_amdgcn_rcpf(1.f - A);
+        const float inv = __builtin_amdgcn_rcpf(T1);
         const float d_live = __builtin_fmaf(inv, P + G0, X);
         const float dal = trans * (term ? X + gA : d_live);
         // u = o*w >= 0, so "u in [0,1]" (the clamp passes the gradient) is ai == u;
