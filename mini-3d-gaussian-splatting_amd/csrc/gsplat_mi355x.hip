@@ -938,7 +938,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   // and dL/dalpha_i = T_i (X_i + (P - K + gA (1 - At)) / T_{i+1}) = T_i (X_i + (P + G0) / T_{i+1}).
   const float K = (gR0 * tr + gR1 * tg) + (gR2 * tbl + gD * Dt);
   const float G0 = __builtin_fmaf(gA, onemA, -K);
-  float P = (gR0 * bg0 + gR1 * bg1) + gR2 * bg2;
+  // PG = P + G0 carried as one running sum (a gradient factor, no decision)
+  float PG = ((gR0 * bg0 + gR1 * bg1) + gR2 * bg2) + G0;
   float A = 0.f, T1 = 1.f;  // T1 = 1 - A, carried: the next entry's transmittance is this one's rcp argument
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   const unsigned long long *lw =
@@ -1080,10 +1081,10 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float trans = T1;
         const float c = trans * (po.y * wv);
         A = A + c;
-        P = __builtin_fmaf(c, X, P);
+        PG = __builtin_fmaf(c, X, PG);
         T1 = 1.f - A;
         const float inv = __builtin_amdgcn_rcpf(T1);  // v_rcp_f32 (1 ulp): a gradient factor, no decision
-        const float d_live = __builtin_fmaf(inv, P + G0, X);
+        const float d_live = __builtin_fmaf(inv, PG, X);
         // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
         const float dal = trans * (A >= kAlphaStop ? X + gA : d_live);
         dop = dal * wv;
@@ -1098,12 +1099,12 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         // +0 for a skipped pair and > 0 for an accepted one (take <=> c > 0)
         const float c = trans * ((live && !(w < kMinWeight)) ? ai : 0.f);
         A = A + c;
-        P = __builtin_fmaf(c, X, P);
+        PG = __builtin_fmaf(c, X, PG);
         const bool term = A >= kAlphaStop;
         T1 = 1.f - A;
         // both arms computed, then a select: no divergent branch per entry
         const float inv = __builtin_amdgcn_rcpf(T1);
-        const float d_live = __builtin_fmaf(inv, P + G0, X);
+        const float d_live = __builtin_fmaf(inv, PG, X);
         const float dal = trans * (term ? X + gA : d_live);
         // u = o*w >= 0, so "u in [0,1]" (the clamp passes the gradient) is ai == u;
         // e = exp(.) >= 0, so "e in [0,1]" is w == e (both false for NaN)
