@@ -22,6 +22,10 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          # between forward and backward, and follow the reference's unfused
          # fp32 order; no contraction of a*b+c into fma.
          "-ffp-contract=off",
+         # no SLP packing of scalar fp32 math into v_pk_add/mul_f32: on gfx950
+         # a packed op costs the issue time of two plain ones plus hazard nops
+         # (measured: blend backward 620 -> 571 us without it)
+         "-fno-slp-vectorize",
          "-Wall", "-Wno-unused-function"]
 
 
