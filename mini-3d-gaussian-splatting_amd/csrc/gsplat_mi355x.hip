@@ -848,7 +848,11 @@ constexpr int kBwdRow = kBwdGroup == 8 ? kWave + 8 : kWave + 16;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  // bound_ctrl: every pattern used here is a full permutation inside a row
+  // (no invalid source lane), so it changes no value -- but it lets the
+  // compiler fold the move into the add (v_add_f32_dpp); without it the
+  // row_half_mirror step became v_mov 0 + v_mov_dpp + v_add
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 // Sum over the 16 lanes of each DPP row; every lane of the row gets the sum.
 __device__ __forceinline__ float row16_sum(float v) {
