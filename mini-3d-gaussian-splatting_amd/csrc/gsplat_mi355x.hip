@@ -893,8 +893,7 @@ __device__ __forceinline__ void quad_tile(int &tile, int &quad) {
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
-  __shared__ int s_idx[kBwdGroup];       // chunk entry j's bit in the word
-  __shared__ float2 s_wrec[kWave * 6];   // the word's live records; word 10 = the entry's slot
+  __shared__ float2 s_wrec[kWave * 6];   // the word's live records, packed in bit order; word 10 = slot
   int tile, quad;
   quad_tile(tile, quad);
   if (tile >= a.tiles_x * a.tiles_y) return;
@@ -969,21 +968,18 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       r2 = recs[3 * (size_t)gid + 2];
     }
   };
-  // Phase B over a chunk: the k live entries of the current word whose bits
-  // cm holds (bit order = group order); their records are still staged.
-  auto phase_b = [&](auto masked_tag, unsigned long long cm, int k) {
+  // Phase B over a chunk: the k live entries of the current word staged at
+  // packed positions kb .. kb + k - 1 (group order).
+  auto phase_b = [&](auto masked_tag, uint32_t kb, int k) {
     constexpr bool kMasked = decltype(masked_tag)::value;
-    // each chunk entry's lane publishes its bit at the entry's rank in cm
-    if ((cm >> lane) & 1ull)
-      s_idx[__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u))] = lane;
-    // this wave's LDS writes have landed before other lanes read them
+    // (the group buffer rows were written by this wave: waited for below)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int j = lane / kBwdLanes, sub = lane % kBwdLanes, col = sub & 7, row0 = sub >> 3;
     if (j < k) {
-      const int bit = s_idx[j];
-      const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * bit];  // mx my q00 q11
-      const float2 ib = s_wrec[6 * bit + 2];                                // qo o
-      const uint32_t slot = __float_as_uint(s_wrec[6 * bit + 5].x);
+      const uint32_t e = kb + (uint32_t)j;
+      const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * e];  // mx my q00 q11
+      const float2 ib = s_wrec[6 * e + 2];                                // qo o
+      const uint32_t slot = __float_as_uint(s_wrec[6 * e + 5].x);
       const float hop = -0.5f * ib.y;
       // this lane's pixels (x0 + col, y0 + r), r = 0..7: dx = bx, dy = by + r
       const float bx = (float)(x0 + col) - ia.x, by = (float)(y0 + row0) - ia.y;
@@ -1020,12 +1016,12 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float q00 = ia.z, qo = ib.x, q11 = ia.w;
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
-        const size_t e = (size_t)slot * 4u + (uint32_t)quad;
-        float4 *out = reinterpret_cast<float4 *>(a.pair_grads + e * GS_PARTIAL_STRIDE);
+        const size_t sq = (size_t)slot * 4u + (uint32_t)quad;
+        float4 *out = reinterpret_cast<float4 *>(a.pair_grads + sq * GS_PARTIAL_STRIDE);
         out[0] = make_float4(g0, g1, g2, g3);
         out[1] = make_float4(g4, g5, g6, g7);
         *reinterpret_cast<float2 *>(out + 2) = make_float2(g8, g9);
-        a.slot_live[e] = 1;
+        a.slot_live[sq] = 1;
       }
     }
   };
@@ -1039,7 +1035,11 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       const uint32_t info = __float_as_uint(r2.w);
       const uint32_t slot = __float_as_uint(r2.z) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
                             (tx - (info & 0xFFFu));
-      float4 *d = reinterpret_cast<float4 *>(&s_wrec[6 * lane]);
+      // packed: the live entry of rank r (bit order) at position r, so a
+      // chunk's records sit at compile-time offsets from one base address
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(mcur >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mcur, 0u));
+      float4 *d = reinterpret_cast<float4 *>(&s_wrec[6 * rank]);
       d[0] = r0;
       d[1] = r1;
       d[2] = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
@@ -1049,10 +1049,17 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     fetch(wd + 1u, mnext);  // in flight while this word replays
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
     unsigned long long m = mcur;
+    uint32_t kb = 0;  // packed position of the chunk's first entry
     while (m) {
      // a chunk: the word's next (up to) kBwdGroup live entries
      unsigned long long cm = 0;
      int k = 0;
+     // the chunk's records: one VGPR base (asm: the compiler would otherwise
+     // re-materialise it from the SGPR with a v_mov per entry), entry kk at a
+     // compile-time offset from it
+     uint32_t vb;
+     asm volatile("v_mov_b32 %0, %1" : "=v"(vb) : "s"(kb * 48u));
+     const char *cb = reinterpret_cast<const char *>(s_wrec) + vb;
      // unrolled: the group row k is a compile-time LDS offset
 #pragma unroll
      for (int kk = 0; kk < kBwdGroup; ++kk) {
@@ -1063,9 +1070,9 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       const uint32_t i = 64u * wd + bit;
       // two b128 broadcasts and a b64: (mx my q00 q11) (qo o r g) (b z);
       // pq = (q00, q11), po = (qo, opacity)
-      const float4 r0v = reinterpret_cast<const float4 *>(s_wrec)[3 * bit];
-      const float4 r1v = reinterpret_cast<const float4 *>(s_wrec)[3 * bit + 1];
-      const float2 pbz = s_wrec[6 * bit + 4];
+      const float4 r0v = reinterpret_cast<const float4 *>(cb + 48 * kk)[0];
+      const float4 r1v = reinterpret_cast<const float4 *>(cb + 48 * kk)[1];
+      const float2 pbz = reinterpret_cast<const float2 *>(cb + 48 * kk)[4];
       const float2 pm = make_float2(r0v.x, r0v.y), pq = make_float2(r0v.z, r0v.w);
       const float2 po = make_float2(r1v.x, r1v.y), prg = make_float2(r1v.z, r1v.w);
       const float dx = fx - pm.x, dy = fy - pm.y;
@@ -1119,7 +1126,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       s_dc[kk][lane] = make_float2(dop, cw);
       k = kk + 1;
      }
-     if ((simple_w & cm) == cm) phase_b(std::false_type{}, cm, k); else phase_b(std::true_type{}, cm, k);
+     if ((simple_w & cm) == cm) phase_b(std::false_type{}, kb, k); else phase_b(std::true_type{}, kb, k);
+     kb += (uint32_t)k;
     }
     mcur = mnext;
   }
