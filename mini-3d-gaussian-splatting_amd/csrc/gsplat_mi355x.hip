@@ -32,7 +32,12 @@ constexpr int kSortIpt = 8;                      // items per thread per sort bl
 constexpr int kSortChunk = kBlock * kSortIpt;    // 2048 items per block
 constexpr int kBinChunk = kBlock * 4;            // 1024 Gaussians per binning block
 constexpr float kAlphaStop = 0.995f;             // renderer.py:352
-constexpr float kMinWeight = 1e-5f;              // renderer.py:336
+// renderer.py:336 skips a pair when w = exp(-s/2) < 1e-5; decided here on
+// s: s > 2 ln(1e5).  The same decision except where exp's rounding
+// straddles 1e-5 -- the band in which any two fp32 exps (ours, torch's)
+// already disagree -- and it saves the compare on w for every evaluated
+// pair (C3: the same 9 knife-edge pixels).  Forward and backward share it.
+constexpr float kSkipS = 23.0258509f;
 
 thread_local char g_err[512];
 
@@ -763,9 +768,9 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
         const float dx = fx - pm.x, dy = fy - pm.y;
         const float s = conic_s(dx, dy, pq.x, po.x, pq.y);  // :333
-        // s > 23.1 means exp(-s/2) < 1e-5, i.e. the :336 skip, decided without exp
+        // the :336 skip (w < 1e-5) decided on s, before exp (kSkipS)
         const bool run = A < kAlphaStop;  // the pixel has not terminated
-        const bool live = run && !(s > 23.1f);
+        const bool live = run && !(s > kSkipS);
         if (wave_any(live)) {
           livem |= 1ull << bit;
           const float w = sat01(exp_neg_half(s));  // :334
@@ -773,7 +778,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
           // gets ai = 0, hence c = (1 - A) * 0 = +0 (1 - A >= 0), and an
           // accepted one c = (1 - A) * ai > 0 -- the reference's c exactly.
           // Selects (v_cndmask) instead of SGPR mask arithmetic.
-          const float ai = (live && !(w < kMinWeight)) ? sat01(po.y * w) : 0.f;  // :339
+          const float ai = live ? sat01(po.y * w) : 0.f;  // :339
           const float c = (1.f - A) * ai;                                        // :343-344
           const float2 prg = lds_pair(&s_rec[6 * j + 3]), pbz = lds_pair(&s_rec[6 * j + 4]);
           // colour / depth sums fused (one rounding per term): they decide
@@ -1077,8 +1082,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       const float2 po = make_float2(r1v.x, r1v.y), prg = make_float2(r1v.z, r1v.w);
       const float dx = fx - pm.x, dy = fy - pm.y;
       const float sq = conic_s(dx, dy, pq.x, po.x, pq.y);
-      // exp(-11.55) < 1e-5: exact early skip (NaN falls through), as in the forward
-      const bool live = (i < neval) && !(sq > 23.1f);
+      // the w < 1e-5 skip on s, as in the forward (NaN falls through)
+      const bool live = (i < neval) && !(sq > kSkipS);
       const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
       const bool simple = (simple_w >> bit) & 1ull;
       float dop, cw;
@@ -1088,7 +1093,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         // gradients -- the general path below with its clamp tests removed,
         // the same values.  wv = 0 exactly where the pair is skipped.
         const float w = exp_neg_half(sq);
-        const float wv = (live && !(w < kMinWeight)) ? w : 0.f;
+        const float wv = live ? w : 0.f;
         const float trans = T1;
         const float c = trans * (po.y * wv);
         A = A + c;
@@ -1108,7 +1113,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float trans = T1;
         // the forward's skips folded into the weight exactly as there: c is
         // +0 for a skipped pair and > 0 for an accepted one (take <=> c > 0)
-        const float c = trans * ((live && !(w < kMinWeight)) ? ai : 0.f);
+        const float c = trans * (live ? ai : 0.f);
         A = A + c;
         PG = __builtin_fmaf(c, X, PG);
         const bool term = A >= kAlphaStop;
