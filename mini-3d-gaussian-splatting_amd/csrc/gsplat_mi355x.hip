@@ -872,6 +872,9 @@ __device__ __forceinline__ float oct_sum(float v) {
   v += dpp_row<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_row<0x4E>(v);   // quad_perm [2,3,0,1]
   v += dpp_row<0x141>(v);  // row_half_mirror: lane x <- lane 7 - x of its 8
+  // (empty asm: keeps the last add next to its DPP move, where the two fold
+  // into one v_add_f32_dpp, instead of being sunk into the storing lane's branch)
+  asm volatile("" : "+v"(v));
   return v;
 }
 
