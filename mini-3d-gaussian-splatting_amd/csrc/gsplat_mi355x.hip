@@ -1056,6 +1056,10 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     const unsigned long long mnext = wd + 1u < nwords ? live_word(wd + 1u) : 0ull;
     fetch(wd + 1u, mnext);  // in flight while this word replays
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
+    // a word whose live entries are all simple (the common case) runs a copy
+    // of the loop without the per-entry test
+    auto run_word = [&](auto all_simple_tag) {
+    constexpr bool kAllSimple = decltype(all_simple_tag)::value;
     unsigned long long m = mcur;
     uint32_t kb = 0;  // packed position of the chunk's first entry
     while (m) {
@@ -1088,7 +1092,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       // the w < 1e-5 skip on s, as in the forward (NaN falls through)
       const bool live = (i < neval) && !(sq > kSkipS);
       const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
-      const bool simple = (simple_w >> bit) & 1ull;
+      const bool simple = kAllSimple || ((simple_w >> bit) & 1ull);
       float dop, cw;
       if (simple) {
         // Fast path (simple_entry): e = exp(-s/2) lies in [0, 1] (s >= 0) and
@@ -1134,9 +1138,11 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       s_dc[kk][lane] = make_float2(dop, cw);
       k = kk + 1;
      }
-     if ((simple_w & cm) == cm) phase_b(std::false_type{}, kb, k); else phase_b(std::true_type{}, kb, k);
+     if (kAllSimple || (simple_w & cm) == cm) phase_b(std::false_type{}, kb, k); else phase_b(std::true_type{}, kb, k);
      kb += (uint32_t)k;
     }
+    };
+    if ((simple_w & mcur) == mcur) run_word(std::true_type{}); else run_word(std::false_type{});
     mcur = mnext;
   }
 }
