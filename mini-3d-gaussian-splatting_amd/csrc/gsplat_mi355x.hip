@@ -1163,22 +1163,41 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
   float2 acc[kF2];
 #pragma unroll
   for (int k = 0; k < kF2; ++k) acc[k] = make_float2(0.f, 0.f);
-  // (vis, rect and first slot in one round trip: the culled have empty rects anyway)
+  // vis, rect and first slot in one round trip (the empty asm keeps the
+  // slot load beside the others: used only under the branch, the compiler
+  // would issue it after the vis test, a second round trip)
   const bool valid = g < a.g.n;
-  const bool vis = valid && a.vis[valid ? g : 0];
+  const uint32_t gi = valid ? (uint32_t)g : 0u;
+  const uint32_t visb = a.vis[gi];
   int tx0, tx1, ty0, ty1;
-  unpack_rect(a.rects, valid ? (uint32_t)g : 0u, tx0, tx1, ty0, ty1);
-  const size_t off = a.pair_offset[valid ? g : 0];
-  if (vis) {
-    const uint32_t cnt = rect_touches(tx0, tx1, ty0, ty1);
+  unpack_rect(a.rects, gi, tx0, tx1, ty0, ty1);
+  uint32_t off32 = a.pair_offset[gi];
+  asm volatile("" : "+v"(off32));
+  const uint32_t cnt = (valid && visb) ? rect_touches(tx0, tx1, ty0, ty1) : 0u;
+  if (cnt > (uint32_t)h) {
+    const size_t off = off32;
     const uint8_t *flag = a.slot_live + off * 4 + q;  // (slot e, q) at flag[4 e]
     // quadrant-q partial of slot e at part[e * 4 * kS4] (48-B records: 16-B loads)
     const float4 *part = reinterpret_cast<const float4 *>(a.pair_grads + (off * 4 + q) * GS_PARTIAL_STRIDE);
     constexpr int kS4 = GS_PARTIAL_STRIDE / 4;
     for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += 8) {
+      // the 4 flags in one round trip: unconditional loads (past the end
+      // the clamped index re-reads slot e0), masked after
       uint32_t f[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) f[i] = e0 + 2 * i < cnt ? flag[4 * (e0 + 2 * i)] : 0u;
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t e = e0 + 2 * i;
+        f[i] = flag[4 * (e < cnt ? e : e0)];
+      }
+      // all four flags tested before any partial is requested: the partial
+      // loads are conditional, so a wait for a later flag placed between them
+      // would have to count them out conservatively and drain them
+      uint32_t fm = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fm |= (e0 + 2 * i < cnt && f[i]) ? 1u << i : 0u;
+      asm volatile("" : "+v"(fm));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) f[i] = (fm >> i) & 1u;
       float4 va[4], vb[4];
       float2 vc[4];
 #pragma unroll
