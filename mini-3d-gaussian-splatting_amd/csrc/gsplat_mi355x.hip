@@ -912,31 +912,44 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   const int W = a.cam.image_width, H = a.cam.image_height;
   const bool inside = px < W && py < H;
   const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]);
+  const uint32_t lend = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
+  const float4 *recs = reinterpret_cast<const float4 *>(a.records);
+  // The prologue's loads in two round trips, without branches (a load under
+  // a branch is waited for at its join): (1) the pixel's state and
+  // cotangents, word 0's liveness word and its entries' Gaussian ids;
+  // (2) speculatively every word-0 entry's record, not only the live ones.
+  // Lanes outside the image / past the list read valid dummies (pixel 0,
+  // entry 0), never used.
+  const unsigned long long *lw =
+      reinterpret_cast<const unsigned long long *>(a.live_bits) + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile;
+  const unsigned long long w0 = lw[0];
+  const uint32_t gid0 = a.sorted_gauss[start + (uint32_t)lane < lend ? start + (uint32_t)lane : 0u];
+  const size_t HW = (size_t)W * H;
+  const size_t p = inside ? (size_t)py * W + px : 0;
+  const float4 acc = reinterpret_cast<const float4 *>(a.pix_acc)[p];
+  const float2 st = reinterpret_cast<const float2 *>(a.pix_state)[p];
+  const float gi0 = a.g_image[p], gi1 = a.g_image[HW + p], gi2 = a.g_image[2 * HW + p];
+  const float gal = (a.g_alpha ? a.g_alpha : a.g_image)[p];
+  const float gdp = (a.g_depth ? a.g_depth : a.g_image)[p];
+  float4 r0 = recs[3 * (size_t)gid0], r1 = recs[3 * (size_t)gid0 + 1], r2 = recs[3 * (size_t)gid0 + 2];
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
   // pixel cotangents through clamp / bg composite / depth normalisation
-  float gR0 = 0.f, gR1 = 0.f, gR2 = 0.f, gA = 0.f, gD = 0.f;
-  float tr = 0.f, tg = 0.f, tbl = 0.f, Dt = 0.f, At = 0.f;
-  uint32_t neval = 0;
-  if (inside) {
-    const size_t HW = (size_t)W * H;
-    const size_t p = (size_t)py * W + px;
-    const float4 acc = reinterpret_cast<const float4 *>(a.pix_acc)[p];
-    const float2 st = reinterpret_cast<const float2 *>(a.pix_state)[p];
-    tr = acc.x; tg = acc.y; tbl = acc.z; Dt = acc.w; At = st.x;
-    neval = __float_as_uint(st.y);
-    const float tb = 1.f - At;
-    const float pr = tr + tb * bg0, pg = tg + tb * bg1, pb = tbl + tb * bg2;
-    gR0 = (pr >= 0.f && pr <= 1.f) ? a.g_image[p] : 0.f;
-    gR1 = (pg >= 0.f && pg <= 1.f) ? a.g_image[HW + p] : 0.f;
-    gR2 = (pb >= 0.f && pb <= 1.f) ? a.g_image[2 * HW + p] : 0.f;
-    gA = -gR0 * bg0 - gR1 * bg1 - gR2 * bg2;
-    if (a.g_alpha && At >= 0.f && At <= 1.f) gA += a.g_alpha[p];
-    if (a.g_depth) {
-      const float den = At + 1e-6f;
-      gD = a.g_depth[p] / den;
-      gA += -a.g_depth[p] * Dt / (den * den);
-    }
-  }
+  // (selects, no branch: the compiler would sink the loads into it)
+  const float tr = inside ? acc.x : 0.f, tg = inside ? acc.y : 0.f, tbl = inside ? acc.z : 0.f;
+  const float Dt = inside ? acc.w : 0.f, At = inside ? st.x : 0.f;
+  const uint32_t neval = inside ? __float_as_uint(st.y) : 0u;
+  const float tb = 1.f - At;
+  const float pr = tr + tb * bg0, pg = tg + tb * bg1, pb = tbl + tb * bg2;
+  const float gR0 = (inside && pr >= 0.f && pr <= 1.f) ? gi0 : 0.f;
+  const float gR1 = (inside && pg >= 0.f && pg <= 1.f) ? gi1 : 0.f;
+  const float gR2 = (inside && pb >= 0.f && pb <= 1.f) ? gi2 : 0.f;
+  float gA = -gR0 * bg0 - gR1 * bg1 - gR2 * bg2;
+  if (inside && a.g_alpha && At >= 0.f && At <= 1.f) gA += gal;
+  const bool has_d = inside && a.g_depth;
+  const float den = At + 1e-6f;
+  const float gD = has_d ? gdp / den : 0.f;
+  const float gAd = -gdp * Dt / (den * den);
+  if (has_d) gA += gAd;
   // the quadrant's last evaluated entry: nothing past it carries gradient here
   const uint32_t wstop = __builtin_amdgcn_readfirstlane(wave_max_u32(neval));
   if (wstop == 0) return;
@@ -952,13 +965,10 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   // PG = P + G0 carried as one running sum (a gradient factor, no decision)
   float PG = ((gR0 * bg0 + gR1 * bg1) + gR2 * bg2) + G0;
   float A = 0.f, T1 = 1.f;  // T1 = 1 - A, carried: the next entry's transmittance is this one's rcp argument
-  const float4 *recs = reinterpret_cast<const float4 *>(a.records);
-  const unsigned long long *lw =
-      reinterpret_cast<const unsigned long long *>(a.live_bits) + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile;
   const uint32_t nwords = (wstop + 63u) >> 6;
   // liveness word wd of this quadrant, cut at wstop (bits past it were never written)
   auto live_word = [&](uint32_t wd) -> unsigned long long {
-    const unsigned long long w = lw[wd];
+    const unsigned long long w = wd == 0 ? w0 : lw[wd];
     // (readfirstlane returns int: widen through uint32_t, never sign-extend)
     const unsigned long long m =
         ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32) |
@@ -966,7 +976,6 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     const uint32_t rem = wstop - 64u * wd;
     return rem < 64u ? m & ((1ull << rem) - 1ull) : m;
   };
-  float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
   // lane l gathers the record of entry 64 wd + l when that entry is live here
   auto fetch = [&](uint32_t wd, unsigned long long m) {
     if ((m >> lane) & 1ull) {
@@ -1033,8 +1042,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       }
     }
   };
-  unsigned long long mcur = live_word(0);
-  fetch(0, mcur);
+  unsigned long long mcur = live_word(0);  // (word 0's records are in flight already)
   for (uint32_t wd = 0; wd < nwords; ++wd) {
     // stage the word's live records; word 10 becomes the entry's gradient
     // slot (the Gaussian's first slot + this tile's index in its rectangle)
