@@ -389,10 +389,19 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restric
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t mask = (1u << nbits) - 1u;
   const long long base = (long long)blockIdx.x * kSortChunk + wave * (kSortChunk / 4);
+  // all rounds' keys in one round trip: unconditional loads (clamped index;
+  // a load under a branch is waited for at its join)
+  uint32_t kr[kSortIpt];
+#pragma unroll
+  for (int r = 0; r < kSortIpt; ++r) {
+    const long long idx = base + r * 64 + lane;
+    kr[r] = keys[idx < n ? idx : n - 1];
+  }
+#pragma unroll
   for (int r = 0; r < kSortIpt; ++r) {
     const long long idx = base + r * 64 + lane;
     const bool valid = idx < n;
-    const uint32_t d = valid ? ((keys[idx] >> shift) & mask) : 0u;
+    const uint32_t d = valid ? ((kr[r] >> shift) & mask) : 0u;
     const unsigned long long m = match_digit(d, nbits, __ballot(valid));
     if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(m));
   }
@@ -416,6 +425,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, uint32_
   if (threadIdx.x == 0) totals[d] = carry;
 }
 
+template <bool kIota>  // values = input positions (the first pass of an iota-valued sort)
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
                                                           const uint32_t *__restrict__ vals_in,
                                                           uint32_t *__restrict__ keys_out,
@@ -430,18 +440,29 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0;
-  uint32_t tot;
-  const uint32_t dbase = block_exscan(totals[threadIdx.x], s_tmp, &tot);  // includes a barrier
   const uint32_t mask = (1u << nbits) - 1u;
   const long long blk0 = (long long)blockIdx.x * kSortChunk;
   const long long base = blk0 + wave * (kSortChunk / 4);
-  uint32_t k_[kSortIpt], v_[kSortIpt], rk[kSortIpt];
+  // all rounds' keys and values in one round trip (unconditional, clamped),
+  // requested before the digit-base scan so that they fly during it
+  uint32_t k_[kSortIpt], v_[kSortIpt];
+#pragma unroll
+  for (int r = 0; r < kSortIpt; ++r) {
+    const long long idx = base + r * 64 + lane;
+    const long long ci = idx < n ? idx : n - 1;
+    k_[r] = keys_in[ci];
+    v_[r] = kIota ? (uint32_t)idx : vals_in[ci];
+  }
+  const uint32_t my_prefix = counts[(size_t)threadIdx.x * nb + blockIdx.x];  // (also in flight)
+  uint32_t tot;
+  const uint32_t dbase = block_exscan(totals[threadIdx.x], s_tmp, &tot);  // includes a barrier
+  uint32_t rk[kSortIpt];
 #pragma unroll
   for (int r = 0; r < kSortIpt; ++r) {
     const long long idx = base + r * 64 + lane;
     const bool valid = idx < n;
-    const uint32_t key = valid ? keys_in[idx] : 0u;
-    const uint32_t val = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+    const uint32_t key = valid ? k_[r] : 0u;
+    const uint32_t val = valid ? v_[r] : 0u;
     const uint32_t d = (key >> shift) & mask;
     const unsigned long long m = match_digit(d, nbits, __ballot(valid));
     const uint32_t below = (uint32_t)__popcll(m & lanemask_lt());
@@ -465,7 +486,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
     }
     const uint32_t lb = block_exscan(run, s_tmp, &tot);  // barrier inside
     s_lbase[threadIdx.x] = lb;
-    s_gbase[threadIdx.x] = dbase + counts[(size_t)threadIdx.x * nb + blockIdx.x];
+    s_gbase[threadIdx.x] = dbase + my_prefix;
   }
   __syncthreads();
   // locally sorted chunk in LDS (stable: wave, round, lane order within a digit)
@@ -1565,8 +1586,10 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
     const int nbits = (end_bit - shift) < kRadixBits ? (end_bit - shift) : kRadixBits;
     k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, nb);
     k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, totals, nb);
-    k_radix_scatter<<<nb, kBlock, 0, s>>>(kin, (p == 0 && vals_are_iota) ? nullptr : vin, kout, vout, n, shift,
-                                          nbits, counts, totals, nb);
+    if (p == 0 && vals_are_iota)
+      k_radix_scatter<true><<<nb, kBlock, 0, s>>>(kin, nullptr, kout, vout, n, shift, nbits, counts, totals, nb);
+    else
+      k_radix_scatter<false><<<nb, kBlock, 0, s>>>(kin, vin, kout, vout, n, shift, nbits, counts, totals, nb);
     gs_status st = check_launch("gs_radix_sort_pairs");
     if (st) return st;
     uint32_t *tk = kin, *tv = vin;
