@@ -415,9 +415,14 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, uint32_
   const int d = blockIdx.x;
   uint32_t *row = counts + (size_t)d * nb;
   uint32_t carry = 0, tot;
+  // the next chunk's load in flight during this chunk's scan (unconditional,
+  // clamped index: no branch for the compiler to wait at)
+  uint32_t vn = row[(int)threadIdx.x < nb ? (int)threadIdx.x : nb - 1];
   for (int c = 0; c < nb; c += kBlock) {
     const int i = c + threadIdx.x;
-    const uint32_t v = i < nb ? row[i] : 0u;
+    const uint32_t v = i < nb ? vn : 0u;
+    const int inext = i + kBlock;
+    vn = row[inext < nb ? inext : nb - 1];
     const uint32_t e = block_exscan(v, s_tmp, &tot);
     if (i < nb) row[i] = carry + e;
     carry += tot;
@@ -516,15 +521,35 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
 __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials, int nb) {
   __shared__ uint32_t s_tmp[4];
   const long long base = (long long)blockIdx.x * kBinChunk;
+  constexpr int kR = kBinChunk / kBlock;
+  // Loads unconditional (clamped index) and all rounds' at once: two round
+  // trips (ids, then their rects/vis) instead of two per round -- a load
+  // under a branch is waited for at the branch's join.  The index-order
+  // rects of the second half are requested here too.
+  uint32_t gi[kR];
+  uint2 rc_own[kR];
+#pragma unroll
+  for (int i = 0; i < kR; ++i) {
+    const long long k = base + i * kBlock + threadIdx.x;
+    const long long kc = k < a.n ? k : a.n - 1;
+    gi[i] = a.sorted_ids[kc];
+    rc_own[i] = reinterpret_cast<const uint2 *>(a.rects)[kc];
+  }
   uint32_t sum = 0, nvis = 0;
-  for (int i = 0; i < kBinChunk / kBlock; ++i) {
+  uint2 rc_d[kR];
+  uint32_t vis_d[kR];
+#pragma unroll
+  for (int i = 0; i < kR; ++i) {
+    rc_d[i] = reinterpret_cast<const uint2 *>(a.rects)[gi[i]];
+    vis_d[i] = a.vis[gi[i]];
+  }
+#pragma unroll
+  for (int i = 0; i < kR; ++i) {
     const long long k = base + i * kBlock + threadIdx.x;
     if (k < a.n) {
-      const uint32_t g = a.sorted_ids[k];
-      int tx0, tx1, ty0, ty1;
-      unpack_rect(a.rects, g, tx0, tx1, ty0, ty1);
-      sum += rect_touches(tx0, tx1, ty0, ty1);
-      nvis += a.vis[g] ? 1u : 0u;
+      sum += rect_touches((int)(rc_d[i].x & 0xFFFFu), (int)(rc_d[i].x >> 16), (int)(rc_d[i].y & 0xFFFFu),
+                          (int)(rc_d[i].y >> 16));
+      nvis += vis_d[i] ? 1u : 0u;
     }
   }
   uint32_t tot, totv;
@@ -539,14 +564,12 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
   // adjacent slot ranges: here each Gaussian's exclusive prefix of touches
   // inside this block's index chunk (k_bin_emit adds the chunk's offset).
   uint32_t carry = 0;
-  for (int i = 0; i < kBinChunk / kBlock; ++i) {
+#pragma unroll
+  for (int i = 0; i < kR; ++i) {
     const long long g = base + i * kBlock + threadIdx.x;
-    uint32_t cnt = 0;
-    if (g < a.n) {
-      int tx0, tx1, ty0, ty1;
-      unpack_rect(a.rects, (uint32_t)g, tx0, tx1, ty0, ty1);
-      cnt = rect_touches(tx0, tx1, ty0, ty1);
-    }
+    const uint32_t cnt = g < a.n ? rect_touches((int)(rc_own[i].x & 0xFFFFu), (int)(rc_own[i].x >> 16),
+                                                (int)(rc_own[i].y & 0xFFFFu), (int)(rc_own[i].y >> 16))
+                                 : 0u;
     uint32_t t;
     const uint32_t ex = block_exscan(cnt, s_tmp, &t);
     if (g < a.n) a.pair_offset[g] = carry + ex;
@@ -601,13 +624,28 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   if ((long long)a.counters[1] > a.capacity) return;
   const long long base = (long long)blockIdx.x * kBinChunk;
   uint32_t out_base = partials[blockIdx.x];
-  for (int r = 0; r < kBinChunk / kBlock; ++r) {
+  constexpr int kR = kBinChunk / kBlock;
+  // all rounds' ids, then their rects, unconditionally (clamped): two round
+  // trips for the block instead of two per round
+  uint32_t gr[kR];
+  uint2 rcr[kR];
+  uint32_t offr[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const long long k = base + r * kBlock + threadIdx.x;
+    gr[r] = a.sorted_ids[k < a.n ? k : a.n - 1];
+    offr[r] = a.pair_offset[k < a.n ? k : a.n - 1];  // (index order, for the slot pass below)
+  }
+#pragma unroll
+  for (int r = 0; r < kR; ++r) rcr[r] = reinterpret_cast<const uint2 *>(a.rects)[gr[r]];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
     const long long k = base + r * kBlock + threadIdx.x;
     uint32_t g = 0xFFFFFFFFu, cnt = 0;
     uint2 rc = make_uint2(1u, 1u);
     if (k < a.n) {
-      g = a.sorted_ids[k];
-      rc = reinterpret_cast<const uint2 *>(a.rects)[g];
+      g = gr[r];
+      rc = rcr[r];
       cnt = rect_touches((int)(rc.x & 0xFFFFu), (int)(rc.x >> 16), (int)(rc.y & 0xFFFFu), (int)(rc.y >> 16));
     }
     uint32_t tot;
@@ -635,10 +673,11 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   // (k_bin_partials); the first slot is also kept in the record (word 10) for
   // the backward.  Records of culled Gaussians are never read.
   const uint32_t cbase = partials[2 * gridDim.x + blockIdx.x];
-  for (int r = 0; r < kBinChunk / kBlock; ++r) {
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
     const long long g = base + r * kBlock + threadIdx.x;
     if (g < a.n) {
-      const uint32_t slot = cbase + a.pair_offset[g];
+      const uint32_t slot = cbase + offr[r];
       a.pair_offset[g] = slot;
       a.records[(size_t)g * GS_RECORD_FLOATS + 10] = __uint_as_float(slot);
     }
