@@ -1297,15 +1297,29 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
   }
 }
 
+// kHot: partials present, no viewspace/conic cotangents, raw scale/rotation,
+// DC colour -- the training configuration.  Its loads are all issued up
+// front (a load under a runtime branch is waited for at the branch's join,
+// which serialised six round trips per thread in the generic instantiation).
+template <bool kHot>
 __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   const int k = blockIdx.x * kBlock + threadIdx.x;
   if (k >= a.g.n) return;
   // in depth order, consecutive threads own adjacent slot ranges
-  const int g = a.order ? (int)a.order[k] : k;
+  const int g = (!kHot && a.order) ? (int)a.order[k] : k;
+  float scl_pre[3] = {0.f, 0.f, 0.f}, rot_pre[4] = {0.f, 0.f, 0.f, 0.f}, op_pre = 0.f;
+  if constexpr (kHot) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) scl_pre[k] = a.g.scaling[(int64_t)g * 3 + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rot_pre[k] = a.g.rotation[(int64_t)g * 4 + k];
+    op_pre = a.g.opacity[(int64_t)g * a.g.opacity_stride];
+  }
+  const float4 Qf = reinterpret_cast<const float4 *>(a.conics)[g];
   float acc[GS_PAIR_GRAD_FLOATS];
 #pragma unroll
   for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
-  if (a.pair_grads) {  // g's partials summed (k_gather_slots)
+  if (kHot || a.pair_grads) {  // g's partials summed (k_gather_slots)
     const float2 *gs = reinterpret_cast<const float2 *>(a.grad_sums) + (size_t)g * (GS_PAIR_GRAD_FLOATS / 2);
 #pragma unroll
     for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) {
@@ -1316,18 +1330,21 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   }
   float dm0 = acc[0], dm1 = acc[1];
   float G[4] = {acc[2], acc[3], acc[3], acc[4]};
-  if (a.g_means2d) {
+  if (!kHot && a.g_means2d) {
     dm0 += a.g_means2d[2 * (size_t)g];
     dm1 += a.g_means2d[2 * (size_t)g + 1];
   }
-  if (a.g_conics) {
+  if (!kHot && a.g_conics) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) G[k] += a.g_conics[4 * (size_t)g + k];
   }
   // colour: sigmoid chain (renderer.py:90), and the SH terms when enabled
   const float *X3 = a.g.xyz + (int64_t)g * a.g.xyz_stride;
   float cl[3], dir[3], inv_norm;
-  color_logits(a.g, a.cam, g, X3[0], X3[1], X3[2], cl, dir, inv_norm);
+  // (the position kept in registers: read again after the stores below, it
+  // would be re-loaded -- the outputs may alias it as far as the compiler knows)
+  const float xw = X3[0], yw = X3[1], zw = X3[2];
+  color_logits(a.g, a.cam, g, xw, yw, zw, cl, dir, inv_norm);
   float dlg[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -1338,7 +1355,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   // SH: d rest_k = Y_k dlogit; the view direction's gradient reaches xyz
   // through dir = v / |v| (added to d_xyz below)
   float dxyz_sh[3] = {0.f, 0.f, 0.f};
-  if (a.g.sh_degree > 0) {
+  if (!kHot && a.g.sh_degree > 0) {
     const int nb = sh_rest_count(a.g.sh_degree);
     const float *r = a.g.sh_rest + (int64_t)g * a.g.sh_rest_stride;
     float Y[15], wY[15];
@@ -1359,13 +1376,13 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   }
   float dop = acc[5];
   if (a.g.opacity_is_logit) {  // through get_opacity's sigmoid, as torch's sigmoid_backward
-    const float o = 1.f / (1.f + expf(-a.g.opacity[(int64_t)g * a.g.opacity_stride]));
+    const float o = 1.f / (1.f + expf(-(kHot ? op_pre : a.g.opacity[(int64_t)g * a.g.opacity_stride])));
     dop = (dop * (1.f - o)) * o;
   }
   a.d_opacity[g] = dop;
   const bool any = dm0 != 0.f || dm1 != 0.f || G[0] != 0.f || G[1] != 0.f || G[2] != 0.f ||
                    G[3] != 0.f || acc[9] != 0.f;
-  const bool raw = a.g.cov3d == nullptr;
+  const bool raw = kHot || a.g.cov3d == nullptr;
   if (!any) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) a.d_xyz[3 * (size_t)g + k] = dxyz_sh[k];
@@ -1395,12 +1412,12 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) Sf[k] = a.g.cov3d[9 * (size_t)g + k];
   } else {
-    cov_from_raw(a.g.scaling + (int64_t)g * 3, a.g.rotation + (int64_t)g * 4, Sf);
+    cov_from_raw(kHot ? scl_pre : a.g.scaling + (int64_t)g * 3, kHot ? rot_pre : a.g.rotation + (int64_t)g * 4, Sf);
   }
   double Xc[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
-    Xc[i] = (double)X3[0] * R[i * 4] + (double)X3[1] * R[i * 4 + 1] + (double)X3[2] * R[i * 4 + 2] + R[i * 4 + 3];
+    Xc[i] = (double)xw * R[i * 4] + (double)yw * R[i * 4 + 1] + (double)zw * R[i * 4 + 2] + R[i * 4 + 3];
   const double X = Xc[0], Y = Xc[1], Z = Xc[2];
   const double fx = c.fx, fy = c.fy;
   double RS[9], C[9];  // C = Rv Sigma Rv^T
@@ -1416,7 +1433,6 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
       C[i * 3 + j] = RS[i * 3] * R[j * 4] + RS[i * 3 + 1] * R[j * 4 + 1] + RS[i * 3 + 2] * R[j * 4 + 2];
   const double iz = 1.0 / Z, iz2 = iz * iz, iz3 = iz2 * iz;
   const double Jd[6] = {fx * iz, 0.0, -fx * X * iz2, 0.0, -fy * iz, fy * Y * iz2};
-  const float4 Qf = reinterpret_cast<const float4 *>(a.conics)[g];
   const double Q[4] = {Qf.x, Qf.y, Qf.z, Qf.w};
   // d cov2d = -Q^T G Q^T (inverse backward)
   const double QG0 = Q[0] * G[0] + Q[2] * G[2], QG1 = Q[0] * G[1] + Q[2] * G[3];
@@ -1474,7 +1490,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
     return;
   }
   // raw path: Sigma = M M^T, M = R(q) diag(s), s = exp(scaling), q = normalize(rotation)
-  const float *sc = a.g.scaling + (int64_t)g * 3, *rq = a.g.rotation + (int64_t)g * 4;
+  const float *sc = kHot ? scl_pre : a.g.scaling + (int64_t)g * 3, *rq = kHot ? rot_pre : a.g.rotation + (int64_t)g * 4;
   float qn = sqrtf(dot3(rq[0], rq[1], rq[2], rq[0], rq[1], rq[2]) + rq[3] * rq[3]);
   qn = qn < 1e-12f ? 1e-12f : qn;
   const float iq = 1.f / qn;
@@ -1728,7 +1744,11 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
                 "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
   if (a->pair_grads) k_gather_slots<<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
-  k_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
+  if (hot)
+    k_project_bwd<true><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  else
+    k_project_bwd<false><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_backward");
 }
 
