@@ -273,6 +273,10 @@ __device__ __forceinline__ void color_logits(const gs_gaussians &G, const gs_cam
 }
 
 // =================================================== stage 1: projection ==
+// kHot: raw scale/rotation and DC colour (training); every input load is
+// issued at the top (under the visibility branch they were waited for in
+// further round trips).
+template <bool kHot>
 __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
   const int g = blockIdx.x * kBlock + threadIdx.x;
   bool visible = false;
@@ -280,13 +284,24 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
     const gs_camera &c = a.cam;
     const float *X3 = a.g.xyz + (int64_t)g * a.g.xyz_stride;
     const float xw = X3[0], yw = X3[1], zw = X3[2];
+    float scl_pre[3] = {0.f, 0.f, 0.f}, rot_pre[4] = {0.f, 0.f, 0.f, 0.f}, cl_pre[3] = {0.f, 0.f, 0.f};
+    float op_pre = 0.f;
+    if constexpr (kHot) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) scl_pre[k] = a.g.scaling[(int64_t)g * 3 + k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) rot_pre[k] = a.g.rotation[(int64_t)g * 4 + k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) cl_pre[k] = a.g.color_logits[(int64_t)g * a.g.color_stride + k];
+      op_pre = a.g.opacity[(int64_t)g * a.g.opacity_stride];
+    }
     float S[9];
-    if (a.g.cov3d) {
+    if (!kHot && a.g.cov3d) {
       const float *cp = a.g.cov3d + (int64_t)g * 9;
 #pragma unroll
       for (int k = 0; k < 9; ++k) S[k] = cp[k];
     } else {
-      cov_from_raw(a.g.scaling + (int64_t)g * 3, a.g.rotation + (int64_t)g * 4, S);
+      cov_from_raw(kHot ? scl_pre : a.g.scaling + (int64_t)g * 3, kHot ? rot_pre : a.g.rotation + (int64_t)g * 4, S);
     }
     const float *R = c.view;  // rows [R | t]
     // Xc = Xw @ Rv.T + Tv (renderer.py:154)
@@ -359,8 +374,13 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
         rinfo = (uint32_t)(x0 / T) | ((uint32_t)(y0 / T) << 12) | ((uint32_t)((x1 - 1) / T - x0 / T) << 24);
       }
       float cl[3], dir[3], inv_norm;
-      color_logits(a.g, c, g, xw, yw, zw, cl, dir, inv_norm);
-      float op = a.g.opacity[(int64_t)g * a.g.opacity_stride];
+      if constexpr (kHot) {
+        cl[0] = cl_pre[0]; cl[1] = cl_pre[1]; cl[2] = cl_pre[2];
+        (void)dir; (void)inv_norm;
+      } else {
+        color_logits(a.g, c, g, xw, yw, zw, cl, dir, inv_norm);
+      }
+      float op = kHot ? op_pre : a.g.opacity[(int64_t)g * a.g.opacity_stride];
       if (a.g.opacity_is_logit) op = 1.f / (1.f + expf(-op));  // get_opacity
       float4 *rec = reinterpret_cast<float4 *>(a.records) + 3 * (int64_t)g;
       // record: mx my q00 q11 | qo o r g | b z off rinfo -- (q00, q11) adjacent so
@@ -1609,7 +1629,10 @@ gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream) {
     return fail(GS_ERR_INVALID_ARG, "%s: need cov3d or scaling+rotation", "gs_project_forward");
   if (a->g.sh_degree < 0 || a->g.sh_degree > 3 || (a->g.sh_degree > 0 && !a->g.sh_rest))
     return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest when > 0", "gs_project_forward");
-  k_project_fwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  if (!a->g.cov3d && a->g.sh_degree == 0)
+    k_project_fwd<true><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  else
+    k_project_fwd<false><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_forward");
 }
 
