@@ -993,6 +993,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   const bool inside = px < W && py < H;
   const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]);
   const uint32_t lend = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
+  if (start >= lend) return;  // empty list: no gradient here (and no entry to read speculatively)
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   // The prologue's loads in two round trips, without branches (a load under
   // a branch is waited for at its join): (1) the pixel's state and
@@ -1743,8 +1744,8 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16", "gs_blend_backward");
   if (a->tiles_x != (int)div_up(a->cam.image_width, GS_TILE) || a->tiles_y != (int)div_up(a->cam.image_height, GS_TILE))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_backward");
-  if (!a->ranges || !a->records || !a->pix_acc || !a->pix_state || !a->g_image || !a->pair_grads ||
-      !a->slot_live || !a->live_bits || a->live_words <= 0)
+  if (!a->ranges || !a->sorted_gauss || !a->records || !a->pix_acc || !a->pix_state || !a->g_image ||
+      !a->pair_grads || !a->slot_live || !a->live_bits || a->live_words <= 0)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_backward");
   hipStream_t s = (hipStream_t)stream;
   const int num_tiles = a->tiles_x * a->tiles_y;
