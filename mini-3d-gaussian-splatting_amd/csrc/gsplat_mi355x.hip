@@ -845,7 +845,12 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
         m &= ~(1ull << bit);
         const uint32_t j = 64u * wd + bit;
         // pq = (q00, q11), po = (qo, opacity)
-        const float2 pm = lds_pair(&s_rec[6 * j]), pq = lds_pair(&s_rec[6 * j + 1]), po = lds_pair(&s_rec[6 * j + 2]);
+        // the entry's LDS address in a pinned VGPR (asm: not re-materialised
+        // from the SGPR for the colour/depth reads below, a VALU saved)
+        uint32_t ja;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(ja) : "s"(j * 48u));
+        const float2 *rj = reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(s_rec) + ja);
+        const float2 pm = lds_pair(rj), pq = lds_pair(rj + 1), po = lds_pair(rj + 2);
         const float dx = fx - pm.x, dy = fy - pm.y;
         const float s = conic_s(dx, dy, pq.x, po.x, pq.y);  // :333
         // the :336 skip (w < 1e-5) decided on s, before exp (kSkipS)
@@ -860,7 +865,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
           // Selects (v_cndmask) instead of SGPR mask arithmetic.
           const float ai = live ? sat01(po.y * w) : 0.f;  // :339
           const float c = (1.f - A) * ai;                                        // :343-344
-          const float2 prg = lds_pair(&s_rec[6 * j + 3]), pbz = lds_pair(&s_rec[6 * j + 4]);
+          const float2 prg = lds_pair(rj + 3), pbz = lds_pair(rj + 4);
           // colour / depth sums fused (one rounding per term): they decide
           // nothing -- termination reads A only -- and the backward reads
           // their totals
