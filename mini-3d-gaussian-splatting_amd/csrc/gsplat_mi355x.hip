@@ -1573,6 +1573,34 @@ __global__ __launch_bounds__(kBlock) void k_adam(gs_adam_args a, int4 firsts0, i
   const float step = t.lr / t.bias_correction1, bc2s = t.bias_correction2_sqrt;
   const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
                      reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
+  if (vec && base + kAdamChunk <= t.numel) {
+    // whole chunk in range (all but a tensor's last block): the four rounds'
+    // loads issued together, no branch between them -- under the per-round
+    // branches below the compiler waited for each round's loads in turn
+    float4 p[4], g[4], m[4], v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t i0 = base + ((int64_t)r * kBlock + threadIdx.x) * 4;
+      p[r] = *reinterpret_cast<const float4 *>(t.param + i0);
+      g[r] = *reinterpret_cast<const float4 *>(t.grad + i0);
+      m[r] = *reinterpret_cast<const float4 *>(t.exp_avg + i0);
+      v[r] = *reinterpret_cast<const float4 *>(t.exp_avg_sq + i0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t i0 = base + ((int64_t)r * kBlock + threadIdx.x) * 4;
+#define GS_ADAM_1(c)                                                          \
+      m[r].c = m[r].c + om1 * (g[r].c - m[r].c);                              \
+      v[r].c = b2 * v[r].c + om2 * (g[r].c * g[r].c);                         \
+      p[r].c -= step * (m[r].c / (sqrtf(v[r].c) / bc2s + a.eps));
+      GS_ADAM_1(x) GS_ADAM_1(y) GS_ADAM_1(z) GS_ADAM_1(w)
+#undef GS_ADAM_1
+      *reinterpret_cast<float4 *>(t.param + i0) = p[r];
+      *reinterpret_cast<float4 *>(t.exp_avg + i0) = m[r];
+      *reinterpret_cast<float4 *>(t.exp_avg_sq + i0) = v[r];
+    }
+    return;
+  }
   for (int r = 0; r < 4; ++r) {
     const int64_t i0 = base + ((int64_t)r * kBlock + threadIdx.x) * 4;
     if (i0 >= t.numel) break;
