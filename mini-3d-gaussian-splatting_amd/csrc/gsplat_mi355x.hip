@@ -601,23 +601,30 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
 // exclusive scan of the touch partials (single block); counters[0] = M, [1] = T
 __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials, int nb, uint32_t *counters) {
   __shared__ uint32_t s_tmp[4];
-  uint32_t carry = 0, vis = 0, tot;
+  uint32_t carry = 0, vis = 0, slots = 0, tot;
+  // a chunk's three partials loaded unconditionally (clamped index) and the
+  // next chunk's in flight during this one's scans: no load waits under a
+  // branch (the compiler waited for each conditional load at its join)
+  auto ld = [&](int i, uint32_t *v) {
+    const int ci = i < nb ? i : nb - 1;
+    v[0] = partials[ci];
+    v[1] = partials[nb + ci];
+    v[2] = partials[2 * nb + ci];
+  };
+  uint32_t vn[3];
+  ld((int)threadIdx.x, vn);
   for (int c = 0; c < nb; c += kBlock) {
     const int i = c + threadIdx.x;
-    const uint32_t v = i < nb ? partials[i] : 0u;
-    const uint32_t e = block_exscan(v, s_tmp, &tot);
-    if (i < nb) partials[i] = carry + e;
+    const uint32_t v0 = i < nb ? vn[0] : 0u, v1 = i < nb ? vn[1] : 0u, v2 = i < nb ? vn[2] : 0u;
+    ld(i + kBlock, vn);
+    const uint32_t e0 = block_exscan(v0, s_tmp, &tot);
+    if (i < nb) partials[i] = carry + e0;
     carry += tot;
-    block_exscan(i < nb ? partials[nb + i] : 0u, s_tmp, &tot);
+    block_exscan(v1, s_tmp, &tot);
     vis += tot;
-  }
-  // index-order slot chunks (k_bin_partials): exclusive offsets in place
-  uint32_t slots = 0;
-  for (int c = 0; c < nb; c += kBlock) {
-    const int i = c + threadIdx.x;
-    const uint32_t v = i < nb ? partials[2 * nb + i] : 0u;
-    const uint32_t e = block_exscan(v, s_tmp, &tot);
-    if (i < nb) partials[2 * nb + i] = slots + e;
+    // index-order slot chunks (k_bin_partials): exclusive offsets in place
+    const uint32_t e2 = block_exscan(v2, s_tmp, &tot);
+    if (i < nb) partials[2 * nb + i] = slots + e2;
     slots += tot;
   }
   if (threadIdx.x == 0) {
