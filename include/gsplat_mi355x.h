@@ -31,14 +31,19 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 6
-#define GS_TILE 16            /* renderer.py:24 tile_size default; the only supported value */
+#define GS_ABI_VERSION 7
+#define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
+#define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
+#define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
+                                 edge L holds gs_tile_quads(L) = ceil(L/8)^2 of them (edge cells
+                                 clipped to the tile); one 64-lane wave renders one cell */
+#define GS_MAX_TILES_AXIS 4096 /* ceil(W/L), ceil(H/L) <= 4096 (12-bit tile coordinates) */
+#define GS_MAX_RECT_TILES 256 /* a Gaussian's tile rectangle spans <= 256 tiles in x: holds for
+                                 any radius_max when ceil(W/L) <= 256, else needs
+                                 ceil((2 floor(radius_max) + 1) / L) + 1 <= 256;
+                                 gs_project_forward returns GS_ERR_UNSUPPORTED otherwise */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
-#define GS_MAX_RECT_TILES 8   /* an AABB spans at most 8 tiles per axis ...            */
-#define GS_MAX_RADIUS 55.0f   /* ... while radius_max <= 55 px (2*55+1 px wide); the
-                                 reference default is 50. gs_project_forward returns
-                                 GS_ERR_UNSUPPORTED for a larger radius_max. */
-#define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian, 8x8 quadrant) gradient partial */
+#define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian, 8x8 cell) gradient partial */
 #define GS_PARTIAL_STRIDE 12   /* floats between partials in pair_grads (10 used; 16-B aligned) */
 #define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2..3] reserved */
 
@@ -62,9 +67,9 @@ typedef struct gs_camera {
   float fx, fy, cx, cy;
   float view[12];        /* row-major 3x4 [R | t] */
   float radius_min;      /* GaussianRenderer(radius_min=0.01) */
-  float radius_max;      /* GaussianRenderer(radius_max=50.0); <= GS_MAX_RADIUS */
+  float radius_max;      /* GaussianRenderer(radius_max=50.0): finite, >= radius_min (see GS_MAX_RECT_TILES) */
   float bg[3];           /* RenderSettings.bg_color */
-  int32_t tile_size;     /* must be GS_TILE */
+  int32_t tile_size;     /* GaussianRenderer(tile_size=16): 1..GS_MAX_TILE */
   float campos[3];       /* camera centre in world coordinates, -R^T t; read only when sh_degree > 0 */
 } gs_camera;
 
@@ -181,7 +186,8 @@ gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream);
  * renderer.py:273-367: per pixel (integer coordinates) front-to-back alpha
  * compositing of its tile's list, termination once A >= 0.995, background
  * composite (bg counted twice, as the reference does), clamps, depth
- * normalisation.  One 256-thread workgroup per 16x16 tile.  pix_state
+ * normalisation.  One 256-thread workgroup per 2x2 cells of a tile (the
+ * whole tile at the default tile_size 16), sharing the tile's list.  pix_state
  * keeps what the backward needs: [H*W] float4 (acc_r, acc_g, acc_b, D) and
  * [H*W] float2 (A, bits of n_eval). */
 typedef struct gs_blend_fwd_args {
@@ -195,29 +201,32 @@ typedef struct gs_blend_fwd_args {
   float *depth;                 /* [H,W]   */
   float *pix_acc;               /* [H*W,4] */
   float *pix_state;             /* [H*W,2] */
-  uint64_t *live_bits;          /* [4, live_words]: see gs_blend_live_words */
+  uint64_t *live_bits;          /* [gs_tile_quads(tile_size), live_words]: see gs_blend_live_words */
   int64_t live_words;
 } gs_blend_fwd_args;
 gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
 
-/* Words per quadrant of the liveness bitmap the forward writes for the
+/* Words per cell of the liveness bitmap the forward writes for the
  * backward: bit i of live_bits[q * live_words + ranges[2t] / 64 + t + i / 64]
  * is set iff list entry i of tile t reached (exp(-s/2) >= 1e-5) some
- * still-running pixel of the tile's 8x8 quadrant q = (qx + 2 qy) -- the
- * backward replays exactly those (entry, quadrant) pairs.  Bits past a
- * quadrant's last evaluated entry are left unwritten. */
+ * still-running pixel of the tile's 8x8 cell q = qx + qy * ceil(L/8)
+ * (pixels [qx*8, qx*8+8) x [qy*8, qy*8+8) from the tile's origin) -- the
+ * backward replays exactly those (entry, cell) pairs.  Bits past a cell's
+ * last evaluated entry are left unwritten. */
 size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles);
+/* Cells per tile: ceil(tile_size / 8)^2 (4 for the default 16); 0 if out of range. */
+int32_t gs_tile_quads(int32_t tile_size);
 
 /* ---- Backward of the blend -------------------------------------------
- * One 64-lane workgroup per (tile, 8x8 quadrant), independent of the
- * others: re-walks each pixel's list front-to-back (bit-identical replay of
- * the forward's decisions) over the entries the forward's liveness bitmap
- * marks for the quadrant, and writes one partial gradient per (entry,
- * quadrant): pair_grads[4e + q] = {dmu_x, dmu_y, dQ00, dQ01(=dQ10), dQ11,
- * d_opacity, d_r, d_g, d_b, d_z} over quadrant q's pixels, and sets
- * slot_live[4e + q] = 1; e = the entry's gradient slot (pair_offset[g] + its
- * tile's index in g's rectangle).  Partials of quadrants that did not replay
- * the entry are not written.  No atomics: deterministic. */
+ * One 64-lane workgroup per (tile, 8x8 cell), independent of the others:
+ * re-walks each pixel's list front-to-back (bit-identical replay of the
+ * forward's decisions) over the entries the forward's liveness bitmap marks
+ * for the cell, and writes one partial gradient per (entry, cell):
+ * pair_grads[Q e + q] = {dmu_x, dmu_y, dQ00, dQ01(=dQ10), dQ11, d_opacity,
+ * d_r, d_g, d_b, d_z} over cell q's pixels, and sets slot_live[Q e + q] = 1;
+ * Q = gs_tile_quads(tile_size), e = the entry's gradient slot (pair_offset[g]
+ * + its tile's index in g's rectangle).  Partials of cells that did not
+ * replay the entry are not written.  No atomics: deterministic. */
 typedef struct gs_blend_bwd_args {
   gs_camera cam;
   int32_t tiles_x, tiles_y;
@@ -231,14 +240,14 @@ typedef struct gs_blend_bwd_args {
   const float *g_depth;         /* [H,W] or NULL */
   const uint64_t *live_bits;    /* the forward's liveness bitmap */
   int64_t live_words;
-  float *pair_grads;            /* [T, 4, GS_PARTIAL_STRIDE] */
-  uint8_t *slot_live;           /* [T, 4], zeroed by the caller */
+  float *pair_grads;            /* [T, Q, GS_PARTIAL_STRIDE], Q = gs_tile_quads(cam.tile_size) */
+  uint8_t *slot_live;           /* [T, Q], zeroed by the caller */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
 
 /* ---- Backward of the projection ----------------------------------------
  * Sums each Gaussian's slot partials (slots [pair_offset[g], pair_offset[g]
- * + touches), the quadrants slot_live flags), adds cotangents on the viewspace_points /
+ * + touches), the cells slot_live flags), adds cotangents on the viewspace_points /
  * conics outputs, and chains through sigmoid(colour), inv(cov2d),
  * J cov_cam J^T, Rv Sigma Rv^T, the perspective Jacobian J(X,Y,Z) and
  * Xc = Rv Xw + Tv (autograd of renderer.py:117-200), and, on the raw path,
@@ -254,7 +263,7 @@ typedef struct gs_project_bwd_args {
   const uint32_t *pair_offset;
   const uint32_t *order;       /* [n] permutation to walk the Gaussians in, or NULL: index order
                                   (slots are numbered in index order, so NULL reads them coalesced) */
-  const float *pair_grads;     /* [T,4,GS_PARTIAL_STRIDE]; may be NULL when T == 0 */
+  const float *pair_grads;     /* [T,Q,GS_PARTIAL_STRIDE]; may be NULL when T == 0 */
   const float *g_means2d;      /* [n,2] or NULL */
   const float *g_conics;       /* [n,4] or NULL */
   float *d_xyz;                /* [n,3] */
@@ -264,7 +273,7 @@ typedef struct gs_project_bwd_args {
   float *d_color_logits;       /* [n,3] */
   float *d_opacity;            /* [n]   */
   float *d_sh_rest;            /* [n,15,3] contiguous, written when g.sh_degree > 0 (zeros past the degree) */
-  const uint8_t *slot_live;    /* [T,4] from gs_blend_backward; required with pair_grads */
+  const uint8_t *slot_live;    /* [T,Q] from gs_blend_backward; required with pair_grads */
   float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS] scratch (g's partials summed); with pair_grads */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);

@@ -368,7 +368,7 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
       x1 = x1 > W ? W : x1;
       y1 = y1 > H ? H : y1;
       if (x0 < x1 && y0 < y1) {
-        const int T = GS_TILE;
+        const int T = c.tile_size;  // GaussianRenderer(tile_size) (:290-293)
         rx = (uint32_t)(x0 / T) | ((uint32_t)((x1 - 1) / T) << 16);
         ry = (uint32_t)(y0 / T) | ((uint32_t)((y1 - 1) / T) << 16);
         rinfo = (uint32_t)(x0 / T) | ((uint32_t)(y0 / T) << 12) | ((uint32_t)((x1 - 1) / T - x0 / T) << 24);
@@ -637,15 +637,17 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
 
 // Emission, coalesced: per round of 256 depth-ordered Gaussians, scan their
 // touch counts into LDS and mark each output position with its Gaussian (a
-// byte per position: at most 256 x GS_MAX_RECT_TILES^2 = 16384 per round);
-// then every thread writes consecutive output entries, looking its Gaussian
-// up in one LDS read (a binary search over the offsets took 8 dependent ones).
+// byte per position, a window of kOwnerCap positions at a time: one window
+// per round unless the round's rectangles average more than 64 tiles); then
+// every thread writes consecutive output entries, looking its Gaussian up in
+// one LDS read (a binary search over the offsets took 8 dependent ones).
+constexpr uint32_t kOwnerCap = kBlock * 64;
 __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials) {
   __shared__ uint32_t s_off[kBlock + 1];
   __shared__ uint32_t s_g[kBlock];
   __shared__ uint2 s_rect[kBlock];
   __shared__ uint32_t s_tmp[4];
-  __shared__ uint8_t s_owner[kBlock * GS_MAX_RECT_TILES * GS_MAX_RECT_TILES];
+  __shared__ uint8_t s_owner[kOwnerCap];
   // T entries do not fit: do nothing (the caller re-emits into T-sized
   // buffers; the slot pass below is not idempotent, so it must run once)
   if ((long long)a.counters[1] > a.capacity) return;
@@ -681,17 +683,23 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
     s_g[threadIdx.x] = g;
     s_rect[threadIdx.x] = rc;
     if (threadIdx.x == 0) s_off[kBlock] = tot;
-    for (uint32_t c = 0; c < cnt; ++c) s_owner[ex + c] = (uint8_t)threadIdx.x;
-    __syncthreads();
-    for (uint32_t o = threadIdx.x; o < tot; o += kBlock) {
-      const int lo = s_owner[o];
-      const uint2 rr = s_rect[lo];
-      const uint32_t tx0 = rr.x & 0xFFFFu, ty0 = rr.y & 0xFFFFu;
-      const uint32_t wt = (rr.x >> 16) - tx0 + 1u;
-      const uint32_t loc = o - s_off[lo];
-      const uint32_t row = loc / wt;
-      a.tile_keys[out_base + o] = (ty0 + row) * (uint32_t)a.tiles_x + tx0 + (loc - row * wt);
-      a.pair_gauss[out_base + o] = s_g[lo];
+    // (tot is block-uniform: every thread runs the same windows)
+    for (uint32_t wb = 0; wb < tot; wb += kOwnerCap) {
+      if (wb) __syncthreads();  // the previous window's owner reads are done
+      const uint32_t lo_c = ex > wb ? ex : wb, hi_c = min(ex + cnt, wb + kOwnerCap);
+      for (uint32_t o = lo_c; o < hi_c; ++o) s_owner[o - wb] = (uint8_t)threadIdx.x;
+      __syncthreads();
+      const uint32_t wend = min(tot, wb + kOwnerCap);
+      for (uint32_t o = wb + threadIdx.x; o < wend; o += kBlock) {
+        const int lo = s_owner[o - wb];
+        const uint2 rr = s_rect[lo];
+        const uint32_t tx0 = rr.x & 0xFFFFu, ty0 = rr.y & 0xFFFFu;
+        const uint32_t wt = (rr.x >> 16) - tx0 + 1u;
+        const uint32_t loc = o - s_off[lo];
+        const uint32_t row = loc / wt;
+        a.tile_keys[out_base + o] = (ty0 + row) * (uint32_t)a.tiles_x + tx0 + (loc - row * wt);
+        a.pair_gauss[out_base + o] = s_g[lo];
+      }
     }
     out_base += tot;
   }
@@ -730,15 +738,19 @@ __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
 }
 
 // ======================================================== blend fwd =======
-// Pixel of thread tid in its 16x16 tile: wave w covers the 8x8 quadrant
-// (w&1, w>>1), lane l the pixel (l&7, l>>3) of it -- compact footprints per
-// wave keep the per-pair branches coherent.
-__device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int &px, int &py) {
-  const int tx = tile % tiles_x, ty = tile / tiles_x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  px = tx * GS_TILE + ((wave & 1) << 3) + (lane & 7);
-  py = ty * GS_TILE + ((wave >> 1) << 3) + (lane >> 3);
-}
+// Cells: a tile of edge L (GaussianRenderer.tile_size) is covered from its
+// origin by QX x QX cells of 8x8 pixels, QX = ceil(L/8) (edge cells clipped
+// to the tile); a wave renders one cell, lane l its pixel (l&7, l>>3) --
+// compact footprints per wave keep the per-pair branches coherent.  A
+// 256-thread forward block renders a 2x2 group of cells of one tile (the
+// whole tile when L = 16), all blending that tile's list: group g of the
+// tile's GX x GX groups (GX = ceil(QX/2)), wave w its cell (w&1, w>>1).
+struct CellGeom {
+  int L, QX, GX;
+  __device__ explicit CellGeom(int tile_size) : L(tile_size), QX((tile_size + 7) >> 3), GX((QX + 1) >> 1) {}
+  __device__ int cells() const { return QX * QX; }
+  __device__ int groups() const { return GX * GX; }
+};
 
 // Wave-level culling of list entries.  Bit q of the result is clear only if
 // every pixel centre of the tile's 8x8 quadrant q = (q&1, q>>1) provably has
@@ -783,27 +795,36 @@ __device__ __forceinline__ float2 lds_pair(const float2 *p) {
 
 __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
   __shared__ float2 s_rec[kBlock * 6];
-  const int tile = blockIdx.x;
-  int px, py;
-  tile_pixel(tile, a.tiles_x, px, py);
+  const CellGeom cg(a.cam.tile_size);
+  const int ng = cg.groups();
+  const int tile = (int)blockIdx.x / ng, grp = (int)blockIdx.x - tile * ng;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int gx = grp % cg.GX, gy = grp / cg.GX;
+  const int qx = 2 * gx + (wave & 1), qy = 2 * gy + (wave >> 1);
+  const int lx = qx * 8 + (lane & 7), ly = qy * 8 + (lane >> 3);  // tile-relative pixel
+  const int tox = (tile % a.tiles_x) * cg.L, toy = (tile / a.tiles_x) * cg.L;
+  const int px = tox + lx, py = toy + ly;
   const int W = a.cam.image_width, H = a.cam.image_height;
-  const bool inside = px < W && py < H;
+  const bool inside = lx < cg.L && ly < cg.L && px < W && py < H;
+  // (a cell past the tile's QX x QX has no pixel inside: its wave is done at once)
+  const int qi = qy * cg.QX + qx;
   const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]),
                  end = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
   float ar = bg0, ag = bg1, ab = bg2;  // out_rgb = bg (renderer.py:273)
   // A lane is done once A >= kAlphaStop (A only grows through accepted
-  // pairs, so that is exactly the :352 break); lanes outside the image start
-  // done.  No loop-carried bool: "done" is one compare, not a mask in SGPRs.
+  // pairs, so that is exactly the :352 break); lanes outside the tile or
+  // image start done.  No loop-carried bool: "done" is one compare, not a
+  // mask in SGPRs.
   float A = inside ? 0.f : 1.f, D = 0.f;
   uint32_t neval = 0;
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   __shared__ uint32_t s_live[4];
-  // s_qm[q][w]: bit i set if entry 64w+i of the batch may reach quadrant q
+  // s_qm[q][w]: bit i set if entry 64w+i of the batch may reach cell q of the group
   __shared__ unsigned long long s_qm[4][4];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const float tx0 = (float)((tile % a.tiles_x) * GS_TILE), ty0 = (float)((tile / a.tiles_x) * GS_TILE);
+  // the group's 16x16 box, for the per-cell culling masks
+  const float tx0 = (float)(tox + 16 * gx), ty0 = (float)(toy + 16 * gy);
   // batch i+1's records are gathered into registers while batch i composites
   float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
   if (start + threadIdx.x < end) {
@@ -889,7 +910,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
       }
       // (only words inside the tile's list: the next tile's words follow)
       if (lane == 0 && b - start + 64u * wd < end - start && live_word0 + wd < (uint64_t)a.live_words)
-        a.live_bits[(size_t)wave * a.live_words + live_word0 + wd] = livem;
+        a.live_bits[(size_t)qi * a.live_words + live_word0 + wd] = livem;
     }
     // all pixels of the tile done? (per-wave ballot -- taken with every lane
     // active, outside the lane-0 branch -- then the 4 wave flags)
@@ -981,28 +1002,32 @@ __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
   return o >= 1e-20f && o <= 1.f && tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det;
 }
 
-// Workgroup b -> (tile, quadrant): b, b+8, b+16, b+24 share an XCD (round-
-// robin dispatch; placement is for speed only), so the four quadrants of a
-// tile read its records through one L2.  Grid: ceil(tiles / 8) * 32.
-__device__ __forceinline__ void quad_tile(int &tile, int &quad) {
-  const uint32_t b = blockIdx.x;
-  quad = (int)((b >> 3) & 3u);
-  tile = (int)((b >> 5) * 8u + (b & 7u));
+// Workgroup b -> (tile, cell): b, b+8, b+16, ... share an XCD (round-robin
+// dispatch; placement is for speed only), so the Q cells of a tile read its
+// records through one L2.  Grid: ceil(tiles / 8) * 8 Q.
+__device__ __forceinline__ void quad_tile(int ncell, int &tile, int &quad) {
+  const uint32_t b = blockIdx.x, grp = b >> 3;
+  const uint32_t q = (uint32_t)ncell;
+  quad = (int)(grp % q);
+  tile = (int)((grp / q) * 8u + (b & 7u));
 }
 
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
   __shared__ float2 s_wrec[kWave * 6];   // the word's live records, packed in bit order; word 10 = slot
+  const CellGeom cg(a.cam.tile_size);
+  const int ncell = cg.cells();
   int tile, quad;
-  quad_tile(tile, quad);
+  quad_tile(ncell, tile, quad);
   if (tile >= a.tiles_x * a.tiles_y) return;
   const int lane = threadIdx.x;
   const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
-  const int x0 = (int)tx * GS_TILE + ((quad & 1) << 3), y0 = (int)ty * GS_TILE + ((quad >> 1) << 3);
+  const int cx0 = (quad % cg.QX) * 8, cy0 = (quad / cg.QX) * 8;  // the cell in its tile
+  const int x0 = (int)tx * cg.L + cx0, y0 = (int)ty * cg.L + cy0;
   const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
   const int W = a.cam.image_width, H = a.cam.image_height;
-  const bool inside = px < W && py < H;
+  const bool inside = cx0 + (lane & 7) < cg.L && cy0 + (lane >> 3) < cg.L && px < W && py < H;
   const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]);
   const uint32_t lend = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
   if (start >= lend) return;  // empty list: no gradient here (and no entry to read speculatively)
@@ -1126,7 +1151,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float q00 = ia.z, qo = ib.x, q11 = ia.w;
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
-        const size_t sq = (size_t)slot * 4u + (uint32_t)quad;
+        const size_t sq = (size_t)slot * (uint32_t)ncell + (uint32_t)quad;
         float4 *out = reinterpret_cast<float4 *>(a.pair_grads + sq * GS_PARTIAL_STRIDE);
         out[0] = make_float4(g0, g1, g2, g3);
         out[1] = make_float4(g4, g5, g6, g7);
@@ -1251,7 +1276,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
 // ======================================================== project bwd =====
 // Sum of each Gaussian's gradient partials: 8 lanes per Gaussian, lane
 // (h, q) walks g's slots h, h+2, h+4, ... of [pair_offset[g], pair_offset[g]
-// + touches) and adds the quadrant-q partials slot_live flags (slot order),
+// + touches) and adds the cell-q (q + 4, ...) partials slot_live flags (slot order),
 // then the 8 lane sums are added in a fixed DPP order -- bitwise
 // reproducible.  The four q lanes of a slot read its 160-B partial record
 // together, and consecutive Gaussians' slots are adjacent (index-order
@@ -1275,12 +1300,14 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
   uint32_t off32 = a.pair_offset[gi];
   asm volatile("" : "+v"(off32));
   const uint32_t cnt = (valid && visb) ? rect_touches(tx0, tx1, ty0, ty1) : 0u;
-  if (cnt > (uint32_t)h) {
+  // lane q sums cells q, q + 4, ... of the tile's Q (one pass when Q = 4)
+  const uint32_t ncell = (uint32_t)CellGeom(a.cam.tile_size).cells();
+  for (uint32_t qc = (uint32_t)q; cnt > (uint32_t)h && qc < ncell; qc += 4) {
     const size_t off = off32;
-    const uint8_t *flag = a.slot_live + off * 4 + q;  // (slot e, q) at flag[4 e]
-    // quadrant-q partial of slot e at part[e * 4 * kS4] (48-B records: 16-B loads)
-    const float4 *part = reinterpret_cast<const float4 *>(a.pair_grads + (off * 4 + q) * GS_PARTIAL_STRIDE);
+    const uint8_t *flag = a.slot_live + off * ncell + qc;  // (slot e, cell qc) at flag[Q e]
+    // cell-qc partial of slot e at part[e * Q * kS4] (48-B records: 16-B loads)
     constexpr int kS4 = GS_PARTIAL_STRIDE / 4;
+    const float4 *part = reinterpret_cast<const float4 *>(a.pair_grads + (off * ncell + qc) * GS_PARTIAL_STRIDE);
     for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += 8) {
       // the 4 flags in one round trip: unconditional loads (past the end
       // the clamped index re-reads slot e0), masked after
@@ -1288,7 +1315,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t e = e0 + 2 * i;
-        f[i] = flag[4 * (e < cnt ? e : e0)];
+        f[i] = flag[(size_t)ncell * (e < cnt ? e : e0)];
       }
       // all four flags tested before any partial is requested: the partial
       // loads are conditional, so a wait for a later flag placed between them
@@ -1303,7 +1330,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
       float2 vc[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float4 *src = part + (size_t)(e0 + 2 * i) * 4 * kS4;
+        const float4 *src = part + (size_t)(e0 + 2 * i) * ncell * kS4;
         va[i] = f[i] ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
         vb[i] = f[i] ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
         vc[i] = f[i] ? *reinterpret_cast<const float2 *>(src + 2) : make_float2(0.f, 0.f);
@@ -1638,9 +1665,30 @@ __global__ __launch_bounds__(kBlock) void k_adam(gs_adam_args a, int4 firsts0, i
   }
 }
 
+int cells_per_tile(int tile_size) {
+  const int qx = (tile_size + GS_QUAD - 1) / GS_QUAD;
+  return qx * qx;
+}
+
+// tile_size in range, image non-empty, tile coordinates fit 12 bits
 bool cam_ok(const gs_camera &c) {
-  return c.tile_size == GS_TILE && c.image_width > 0 && c.image_height > 0 &&
-         c.image_width <= (GS_TILE << 12) && c.image_height <= (GS_TILE << 12);
+  if (c.tile_size < 1 || c.tile_size > GS_MAX_TILE || c.image_width <= 0 || c.image_height <= 0) return false;
+  return div_up(c.image_width, c.tile_size) <= GS_MAX_TILES_AXIS && div_up(c.image_height, c.tile_size) <= GS_MAX_TILES_AXIS;
+}
+const char *kCamMsg = "%s: tile_size must be in [1, 256], the image non-empty with at most 4096 tiles per axis";
+
+// A Gaussian's rectangle is at most 2 floor(r) + 1 <= 2 floor(radius_max) + 1
+// pixels wide (renderer.py:278-293), clipped to the image: its tile width
+// minus one must fit the record's 8-bit field (GS_MAX_RECT_TILES).
+bool rect_ok(const gs_camera &c) {
+  if (!(c.radius_max >= 0.f) || !(c.radius_max < 1e9f) || !(c.radius_min <= c.radius_max)) return false;
+  const long long tiles_x = div_up(c.image_width, c.tile_size);
+  const long long span = (2LL * (long long)c.radius_max + 1 + c.tile_size - 1) / c.tile_size + 1;
+  return (span < tiles_x ? span : tiles_x) <= GS_MAX_RECT_TILES;
+}
+
+bool tiles_match(const gs_camera &c, int tiles_x, int tiles_y) {
+  return tiles_x == (int)div_up(c.image_width, c.tile_size) && tiles_y == (int)div_up(c.image_height, c.tile_size);
 }
 
 }  // namespace
@@ -1657,9 +1705,10 @@ const char *gs_last_error(void) { return g_err; }
 
 gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_project_forward");
-  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16 and image size positive", "gs_project_forward");
-  if (!(a->cam.radius_max <= GS_MAX_RADIUS))  // rects wider than GS_MAX_RECT_TILES (k_bin_emit's LDS map)
-    return fail(GS_ERR_UNSUPPORTED, "%s: radius_max must be <= GS_MAX_RADIUS (55 px)", "gs_project_forward");
+  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_project_forward");
+  if (!rect_ok(a->cam))
+    return fail(GS_ERR_UNSUPPORTED, "%s: radius_min <= radius_max, finite, with rectangles of at most 256 tiles in x "
+                "(GS_MAX_RECT_TILES)", "gs_project_forward");
   if (a->g.n < 0) return fail(GS_ERR_INVALID_ARG, "%s: bad n", "gs_project_forward");
   hipStream_t s = (hipStream_t)stream;
   if (a->g.n == 0) return GS_OK;
@@ -1761,6 +1810,10 @@ gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream) {
   return check_launch("gs_tile_ranges");
 }
 
+int32_t gs_tile_quads(int32_t tile_size) {
+  return (tile_size < 1 || tile_size > GS_MAX_TILE) ? 0 : cells_per_tile(tile_size);
+}
+
 size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles) {
   if (num_pairs < 0 || num_tiles < 0) return 0;
   return (size_t)num_pairs / 64u + (size_t)num_tiles + 2u;
@@ -1768,21 +1821,25 @@ size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles) {
 
 gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_forward");
-  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16", "gs_blend_forward");
-  if (a->tiles_x != (int)div_up(a->cam.image_width, GS_TILE) || a->tiles_y != (int)div_up(a->cam.image_height, GS_TILE))
+  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_blend_forward");
+  if (!tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_forward");
   if (!a->ranges || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_acc || !a->pix_state ||
       !a->live_bits || a->live_words <= 0)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_forward");
   hipStream_t s = (hipStream_t)stream;
-  k_blend_fwd<<<a->tiles_x * a->tiles_y, kBlock, 0, s>>>(*a);
+  const int gx = ((a->cam.tile_size + GS_QUAD - 1) / GS_QUAD + 1) / 2;  // 2x2 cell groups per tile axis
+  const long long blocks = (long long)a->tiles_x * a->tiles_y * gx * gx;
+  if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_forward");
+  if (blocks == 0) return GS_OK;
+  k_blend_fwd<<<(unsigned)blocks, kBlock, 0, s>>>(*a);
   return check_launch("gs_blend_forward");
 }
 
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_backward");
-  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, "%s: tile_size must be 16", "gs_blend_backward");
-  if (a->tiles_x != (int)div_up(a->cam.image_width, GS_TILE) || a->tiles_y != (int)div_up(a->cam.image_height, GS_TILE))
+  if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_blend_backward");
+  if (!tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_backward");
   if (!a->ranges || !a->sorted_gauss || !a->records || !a->pix_acc || !a->pix_state || !a->g_image ||
       !a->pair_grads || !a->slot_live || !a->live_bits || a->live_words <= 0)
@@ -1790,7 +1847,9 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const int num_tiles = a->tiles_x * a->tiles_y;
   if (num_tiles <= 0) return GS_OK;
-  k_blend_bwd<<<div_up(num_tiles, 8) * 32u, kWave, 0, s>>>(*a);
+  const long long blocks = (long long)div_up(num_tiles, 8) * 8LL * cells_per_tile(a->cam.tile_size);
+  if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_backward");
+  k_blend_bwd<<<(unsigned)blocks, kWave, 0, s>>>(*a);
   return check_launch("gs_blend_backward");
 }
 
@@ -1806,6 +1865,7 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   if (a->g.sh_degree < 0 || a->g.sh_degree > 3 || (a->g.sh_degree > 0 && (!a->g.sh_rest || !a->d_sh_rest)))
     return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest and d_sh_rest when > 0",
                 "gs_project_backward");
+  if (a->pair_grads && !cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
   if (a->pair_grads) k_gather_slots<<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
   const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;

@@ -39,14 +39,21 @@ class CameraParams:
     bg: Tuple[float, float, float]
     radius_min: float = 0.01
     radius_max: float = 50.0
+    tile_size: int = N.GS_DEFAULT_TILE  # GaussianRenderer(tile_size) (renderer.py:24,261-264)
 
     @property
     def tiles_x(self) -> int:
-        return (self.image_width + N.GS_TILE - 1) // N.GS_TILE
+        return (self.image_width + self.tile_size - 1) // self.tile_size
 
     @property
     def tiles_y(self) -> int:
-        return (self.image_height + N.GS_TILE - 1) // N.GS_TILE
+        return (self.image_height + self.tile_size - 1) // self.tile_size
+
+    @property
+    def cells(self) -> int:
+        """8x8 pixel cells per tile (gs_tile_quads): 4 at the default 16."""
+        q = (self.tile_size + N.GS_QUAD - 1) // N.GS_QUAD
+        return q * q
 
     def to_struct(self) -> N.GsCamera:
         c = N.GsCamera()
@@ -55,7 +62,7 @@ class CameraParams:
         c.view = (C.c_float * 12)(*self.view)
         c.radius_min, c.radius_max = self.radius_min, self.radius_max
         c.bg = (C.c_float * 3)(*self.bg)
-        c.tile_size = N.GS_TILE
+        c.tile_size = int(self.tile_size)
         c.campos = (C.c_float * 3)(*self.campos)
         return c
 
@@ -145,13 +152,13 @@ _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess
 _HOST_COUNTERS: dict = {}  # device -> pinned int32[2] for the (M, T) read-back
 
 
-def _alloc_tile_buffers(lib, cap: int, num_tiles: int, dev):
+def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cells: int, dev):
     """One byte buffer for T <= cap entries: tile keys + Gaussian ids
     (ping-pong, 16 B/entry), the tile sort's workspace and the liveness
-    bitmap (4 x gs_blend_live_words)."""
+    bitmap (cells x gs_blend_live_words)."""
     nbytes = (16 * cap + 255) // 256 * 256
     nbytes += (int(lib.gs_radix_sort_workspace_bytes(cap)) + 255) // 256 * 256
-    nbytes += 32 * int(lib.gs_blend_live_words(cap, num_tiles))
+    nbytes += 8 * cells * int(lib.gs_blend_live_words(cap, num_tiles))
     return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
 
 
@@ -211,7 +218,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         # drops entries past the capacity): its kernel time hides the
         # read-back's round trip.  T above the guess: re-allocate, re-emit.
         cap = _T_SEEN.get(dev, 0)
-        big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, dev) if cap else None
+        big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, cam.cells, dev) if cap else None
         # (M, T) read back through pinned memory, copied BEFORE the emission
         # is queued, so the host wakes while the GPU still emits
         host = _HOST_COUNTERS.get(dev)
@@ -247,7 +254,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     # so this span does no torch work (views of the sorted ids and the bitmap
     # are made after the blend is queued).
     emitted = big_guess is not None and big_guess[1] >= T
-    big, cap_t = big_guess if emitted else _alloc_tile_buffers(lib, T, num_tiles, dev)
+    big, cap_t = big_guess if emitted else _alloc_tile_buffers(lib, T, num_tiles, cam.cells, dev)
     tws_bytes = int(lib.gs_radix_sort_workspace_bytes(T))
     live_words = int(lib.gs_blend_live_words(T, num_tiles))
     base = big.data_ptr()
@@ -280,7 +287,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     # (the blend is queued: views for the frame cost no GPU idle time now)
     kv = big[:16 * cap_t].view(i32).view(4, cap_t)
     fr.sorted_gauss = kv[2 + alt.value, :T]
-    fr.live_bits = big[o_live:o_live + 32 * live_words].view(torch.int64).view(4, live_words)
+    fr.live_bits = big[o_live:o_live + 8 * cam.cells * live_words].view(torch.int64).view(cam.cells, live_words)
     fr.big = big
     fr.pair_offset, fr.ranges = pair_offset, ranges
     fr.pix_acc, fr.pix_state = pix_acc, pix_state
@@ -307,10 +314,10 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_image = g_image.contiguous()
         g_alpha = None if g_alpha is None else g_alpha.contiguous()
         g_depth = None if g_depth is None else g_depth.contiguous()
-        # one partial per (slot, 8x8 quadrant); only the quadrants that replay
-        # an entry write theirs and set its flag
-        pair_grads = torch.empty((fr.T * 4, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
-        slot_live = torch.zeros((fr.T * 4,), dtype=torch.uint8, device=dev)
+        # one partial per (slot, 8x8 cell of the tile); only the cells that
+        # replay an entry write theirs and set its flag
+        pair_grads = torch.empty((fr.T * cam.cells, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
+        slot_live = torch.zeros((fr.T * cam.cells,), dtype=torch.uint8, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),

@@ -59,7 +59,7 @@ def _world_view(camera) -> torch.Tensor:
     return torch.as_tensor(wv)
 
 
-def camera_params(camera, settings: RenderSettings, radius_min=0.01, radius_max=50.0) -> CameraParams:
+def camera_params(camera, settings: RenderSettings, radius_min=0.01, radius_max=50.0, tile_size=16) -> CameraParams:
     """Host scalars of renderer.py:140-152 (python double -> fp32 in the ABI)."""
     W, H = camera._width, camera._height
     fx = 0.5 * W / math.tan(camera._FoVx * 0.5)
@@ -69,22 +69,26 @@ def camera_params(camera, settings: RenderSettings, radius_min=0.01, radius_max=
     bg = settings.bg_color
     bg = tuple(float(v) for v in torch.as_tensor(bg).detach().to("cpu", torch.float32).reshape(3).tolist())
     return CameraParams(int(settings.image_width), int(settings.image_height), fx, fy, W * 0.5, H * 0.5,
-                        view, bg, float(radius_min), float(radius_max))
+                        view, bg, float(radius_min), float(radius_max), int(tile_size))
 
 
 class GaussianRenderer:
     """renderer.py:22-114"""
 
     def __init__(self, tile_size=16, radius_min=0.01, radius_max=50.0):
-        if tile_size != 16:
-            raise ValueError("the MI355X rasterizer implements tile_size=16 (the reference default)")
-        self.tile_size = tile_size
+        # any tile edge the reference's binning can use (renderer.py:261-298),
+        # capped at GS_MAX_TILE; radii as the reference clamps them (:190)
+        if int(tile_size) != tile_size or not 1 <= tile_size <= 256:
+            raise ValueError(f"tile_size must be an integer in [1, 256], got {tile_size!r}")
+        if not (math.isfinite(radius_max) and 0 <= radius_min <= radius_max):
+            raise ValueError(f"need 0 <= radius_min <= radius_max < inf, got {radius_min!r}, {radius_max!r}")
+        self.tile_size = int(tile_size)
         self.radius_min = radius_min
         self.radius_max = radius_max
         self.device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
 
     def render(self, camera, gaussians, settings: RenderSettings) -> Dict[str, torch.Tensor]:
-        cam = camera_params(camera, settings, self.radius_min, self.radius_max)
+        cam = camera_params(camera, settings, self.radius_min, self.radius_max, self.tile_size)
         xyz = gaussians.get_xyz
         fused = getattr(gaussians, "_gs_fused_covariance", False)
         if fused:

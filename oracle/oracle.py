@@ -41,7 +41,7 @@ class _FwdOut(C.Structure):
         ("radii", _fp), ("vis", C.POINTER(C.c_uint8)),
         ("sorted_idx", C.POINTER(C.c_int32)), ("M", C.c_int32),
         ("image", _fp), ("alpha", _fp), ("depth", _fp),
-        ("T", C.c_int64), ("E", C.c_int64), ("C", C.c_int64),
+        ("T", C.c_int64), ("E", C.c_int64), ("C", C.c_int64), ("margin", _fp),
     ]
 
 
@@ -120,7 +120,7 @@ def _scene_struct(s: Scene, keep: list) -> _Scene:
                   _p(arrs["xyz"]), _p(arrs["cov3d"]), _p(arrs["color_logits"]), _p(arrs["opacity"]))
 
 
-def _alloc_fwd(n: int, h: int, w: int):
+def _alloc_fwd(n: int, h: int, w: int, margins: bool = False):
     o = dict(
         means2d=np.zeros((n, 2), np.float32), cov2d=np.zeros((n, 2, 2), np.float32),
         conics=np.zeros((n, 2, 2), np.float32), depths=np.zeros(n, np.float32),
@@ -131,7 +131,10 @@ def _alloc_fwd(n: int, h: int, w: int):
     st = _FwdOut(_p(o["means2d"]), _p(o["cov2d"]), _p(o["conics"]), _p(o["depths"]),
                  _p(o["radii"]), o["vis"].ctypes.data_as(C.POINTER(C.c_uint8)),
                  o["sorted_idx"].ctypes.data_as(C.POINTER(C.c_int32)), 0,
-                 _p(o["image"]), _p(o["alpha"]), _p(o["depth"]), 0, 0, 0)
+                 _p(o["image"]), _p(o["alpha"]), _p(o["depth"]), 0, 0, 0, C.cast(None, _fp))
+    if margins:
+        o["margin"] = np.zeros((2, h, w), np.float32)
+        st.margin = _p(o["margin"])
     return o, st
 
 
@@ -142,11 +145,13 @@ def _finish_fwd(o: dict, st: _FwdOut) -> Dict[str, np.ndarray]:
     return o
 
 
-def render_forward(s: Scene, nthreads: int = 0) -> Dict[str, np.ndarray]:
-    """Forward of renderer.py:31-114; returns numpy arrays + work counters."""
+def render_forward(s: Scene, nthreads: int = 0, margins: bool = False) -> Dict[str, np.ndarray]:
+    """Forward of renderer.py:31-114; returns numpy arrays + work counters.
+    margins: also `margin` [2,H,W], each pixel's distance (ulps) to the w < 1e-5
+    skip and the A >= 0.995 break (gs_oracle.c, gso_fwd_out.margin)."""
     keep: list = []
     sc = _scene_struct(s, keep)
-    o, st = _alloc_fwd(sc.N, s.height, s.width)
+    o, st = _alloc_fwd(sc.N, s.height, s.width, margins)
     rc = lib().gso_forward(C.byref(sc), C.byref(st), int(nthreads))
     if rc:
         raise RuntimeError(f"gso_forward failed ({rc})")
@@ -154,13 +159,13 @@ def render_forward(s: Scene, nthreads: int = 0) -> Dict[str, np.ndarray]:
 
 
 def render_backward(s: Scene, g_image, g_alpha, g_depth, g_means2d=None, g_conics=None,
-                    nthreads: int = 0) -> Dict[str, np.ndarray]:
+                    nthreads: int = 0, margins: bool = False) -> Dict[str, np.ndarray]:
     """Gradients of L = <g_image,image> + <g_alpha,alpha> + <g_depth,depth>
     (+ <g_means2d,viewspace_points> + <g_conics,conics>) w.r.t. the inputs."""
     keep: list = []
     sc = _scene_struct(s, keep)
     n, h, w = sc.N, s.height, s.width
-    o, st = _alloc_fwd(n, h, w)
+    o, st = _alloc_fwd(n, h, w, margins)
     gi, ga, gd = _f32(g_image).reshape(3, h, w), _f32(g_alpha).reshape(h, w), _f32(g_depth).reshape(h, w)
     gm = None if g_means2d is None else _f32(g_means2d).reshape(n, 2)
     gc = None if g_conics is None else _f32(g_conics).reshape(n, 4)

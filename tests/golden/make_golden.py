@@ -140,20 +140,23 @@ def quat_to_R(q):
 
 
 def run_case(ref, name, xyz, cov, logits, opac, wv, W, H, fovx, fovy, bg, cam_wh=None,
-             backward=True, extra_cot=False, seed=1, model=None):
+             backward=True, extra_cot=False, seed=1, model=None, tile=16, radius_min=0.01, radius_max=50.0):
     from src.core.renderer import GaussianRenderer, RenderSettings
     cw, ch = cam_wh if cam_wh is not None else (W, H)
     cam = StubCamera(cw, ch, fovx, fovy, torch.tensor(np.asarray(wv, np.float32)))
     gs = ModelAdapter(model) if model is not None else StubGaussians(xyz, cov, logits, opac)
     settings = RenderSettings(image_height=H, image_width=W,
                               bg_color=torch.tensor(np.asarray(bg, np.float32)))
-    rend = GaussianRenderer(tile_size=16, radius_min=0.01, radius_max=50.0)
+    # the constructor's full range (renderer.py:24-28): tile_size changes the
+    # image (a pixel blends its whole tile's list), radius_max/min the binning
+    rend = GaussianRenderer(tile_size=tile, radius_min=radius_min, radius_max=radius_max)
     t0 = time.time()
     out = rend.render(cam, gs, settings)
     t_fwd = time.time() - t0
     rec = dict(
         width=W, height=H, cam_width=cw, cam_height=ch, fovx=fovx, fovy=fovy,
         wv=np.asarray(wv, np.float32), bg=np.asarray(bg, np.float32),
+        tile=int(tile), radius_min=float(radius_min), radius_max=float(radius_max),
         image=out["image"].detach().numpy(), alpha=out["alpha"].detach().numpy(),
         depth=out["depth"].detach().numpy(), means2d=out["viewspace_points"].detach().numpy(),
         conics=out["conics"].detach().numpy(), radii=out["radii"].detach().numpy(),
@@ -201,7 +204,8 @@ def run_case(ref, name, xyz, cov, logits, opac, wv, W, H, fovx, fovy, bg, cam_wh
                        d_color_logits=z(gs.feats, (n, 16, 3))[:, 0, :],
                        d_opacity=z(gs.op, (n, 1))[:, 0])
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **rec)
-    return dict(name=name, N=int(rec["xyz"].shape[0]), W=W, H=H, backward=backward,
+    return dict(name=name, N=int(rec["xyz"].shape[0]), W=W, H=H, backward=backward, tile=int(tile),
+                radius_max=float(radius_max),
                 ref_fwd_s=round(t_fwd, 3), ref_bwd_s=round(t_bwd, 3),
                 visible=int(rec["vis"].sum()))
 
@@ -303,6 +307,29 @@ def cases(ref, only=None, skip_large=False):
         fx, fy = fov_pair(64, 64, 60.0)
         out.append(run_case(ref, "model_random", None, None, None, None, ident, 64, 64, fx, fy,
                             [0, 0, 0], model=m))
+    # 11-14. GaussianRenderer(tile_size=..., radius_min/max=...) beyond the
+    # defaults: the tile a pixel belongs to decides which Gaussians it blends
+    # (pixels outside a Gaussian's AABB but inside a touched tile still blend it)
+    if want("tile8"):
+        rng = np.random.default_rng(11)
+        xyz, cov, lg, op, fx, fy = synth(60, 64, 64, rng, slo=0.01, shi=0.05)
+        out.append(run_case(ref, "tile8", xyz, cov, lg, op, ident, 64, 64, fx, fy, [0.2, 0.3, 0.4],
+                            extra_cot=True, tile=8))
+    if want("tile32"):
+        rng = np.random.default_rng(12)
+        xyz, cov, lg, op, fx, fy = synth(70, 72, 56, rng, slo=0.01, shi=0.06)
+        out.append(run_case(ref, "tile32", xyz, cov, lg, op, ident, 72, 56, fx, fy, [0.1, 0.0, 0.2], tile=32))
+    if want("tile12"):
+        rng = np.random.default_rng(13)
+        xyz, cov, lg, op, fx, fy = synth(50, 52, 44, rng, slo=0.01, shi=0.05)
+        out.append(run_case(ref, "tile12", xyz, cov, lg, op, ident, 52, 44, fx, fy, [0.0, 0.1, 0.0], tile=12))
+    if want("radius80_tile8"):
+        # 3 sigma beyond 80 px: the clamp binds at radius_max=80, and rects span
+        # 12 x 10 tiles of 8 px (more than the 8 x 8 of the default setup)
+        rng = np.random.default_rng(14)
+        xyz, cov, lg, op, fx, fy = synth(6, 96, 80, rng, zlo=2.0, zhi=3.0, slo=0.7, shi=1.2)
+        out.append(run_case(ref, "radius80_tile8", xyz, cov, lg, op * 0.3, ident, 96, 80, fx, fy,
+                            [0.1, 0.1, 0.1], tile=8, radius_min=0.6, radius_max=80.0))
     # 10. C1-shaped forward only (5k Gaussians, 256x256, SURVEY 8d distribution)
     if want("c1_forward") and not skip_large:
         rng = np.random.default_rng(0)

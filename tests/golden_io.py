@@ -5,6 +5,11 @@ Tolerances (north_star: outputs within 1e-4 fp32 of the reference):
   * conics: rel 1e-4 (entries scale like 1/sigma_px^2)
   * depth = D / (A + 1e-6): abs 1e-4 where alpha >= 1e-2, abs 1e-4 * depth
     scale elsewhere (the division amplifies rounding for tiny A)
+  * scenes checked against the oracle (no reference run possible at that
+    size) may exempt KNIFE-EDGE pixels only: pixels whose oracle replay
+    came within a few ulps of a decision threshold (knife_edge below; the
+    GPU's exp is ~1 ulp from glibc's, so such a pixel may decide the
+    other way), each one reported
   * gradients: |d - d_ref| <= 2e-3 * max|d_ref| + 1e-5 per tensor
     (reference backward is autograd over a different but algebraically
     identical expression order)
@@ -45,7 +50,15 @@ def scene_of(f):
     return o.Scene(xyz=f["xyz"], cov3d=f["cov3d"], color_logits=f["color_logits"],
                    opacity=f["opacity"], wv=f["wv"], width=int(f["width"]), height=int(f["height"]),
                    fovx=float(f["fovx"]), fovy=float(f["fovy"]), bg=f["bg"],
-                   cam_width=int(f["cam_width"]), cam_height=int(f["cam_height"]))
+                   cam_width=int(f["cam_width"]), cam_height=int(f["cam_height"]), **renderer_kwargs(f, "tile"))
+
+
+def renderer_kwargs(f, tile_key="tile_size"):
+    """The fixture's GaussianRenderer(tile_size, radius_min, radius_max)
+    (defaults 16, 0.01, 50 for fixtures that predate the keys)."""
+    return {tile_key: int(f["tile"]) if "tile" in f else 16,
+            "radius_min": float(f["radius_min"]) if "radius_min" in f else 0.01,
+            "radius_max": float(f["radius_max"]) if "radius_max" in f else 50.0}
 
 
 def max_err(a, b):
@@ -56,22 +69,45 @@ def max_err(a, b):
     return float(np.max(np.abs(a - b)))
 
 
-def check_image(out, ref, atol=IMG_ATOL):
-    """Returns a list of failure strings (empty = pass)."""
-    errs = []
-    for k in ("image", "alpha"):
-        e = max_err(out[k], ref[k])
-        if not e <= atol:
-            errs.append(f"{k}: max abs err {e:.3g} > {atol}")
-    a = np.asarray(ref["alpha"], np.float64)
-    d_out = np.asarray(out["depth"], np.float64)
-    d_ref = np.asarray(ref["depth"], np.float64)
+# knife-edge thresholds, in ulps of the threshold value (gso_fwd_out.margin):
+# the w < 1e-5 skip flips only within exp's rounding (~2 ulps of w) -- a
+# flipped pair moves A by <= 1e-5 and depth by <= 1e-5 / A x its depth gap,
+# and may cascade into the break; A at the 0.995 break differs by a few ulps
+# when nothing but exp's rounding differs
+KNIFE_W_ULPS = 4.0
+KNIFE_A_ULPS = 16.0
+
+
+def knife_edge(margin):
+    """[H,W] bool: pixels within rounding of a blend decision."""
+    return (np.asarray(margin[1]) <= KNIFE_A_ULPS) | (np.asarray(margin[0]) <= KNIFE_W_ULPS)
+
+
+def pixel_errors(out, ref, atol=IMG_ATOL):
+    """[H,W] bool: pixels whose image/alpha (abs atol) or depth (abs atol where
+    alpha >= 1e-2, atol x depth scale x 100 elsewhere) is out of tolerance."""
+    img = np.abs(np.asarray(out["image"], np.float64) - np.asarray(ref["image"], np.float64)) > atol
+    bad = img.any(0) | (np.abs(np.asarray(out["alpha"], np.float64) - np.asarray(ref["alpha"], np.float64)) > atol)[0]
+    a = np.asarray(ref["alpha"], np.float64)[0]
+    d_out = np.asarray(out["depth"], np.float64)[0]
+    d_ref = np.asarray(ref["depth"], np.float64)[0]
     scale = max(1.0, float(np.max(np.abs(d_ref))) if d_ref.size else 1.0)
-    tol = np.where(a >= 1e-2, atol * scale, atol * scale * 100)
-    bad = np.abs(d_out - d_ref) > tol
+    tol = np.where(a >= 1e-2, atol, atol * scale * 100)
+    return bad | (np.abs(d_out - d_ref) > tol)
+
+
+def check_image(out, ref, atol=IMG_ATOL, exempt=None):
+    """Returns a list of failure strings (empty = pass).  exempt: optional
+    [H,W] bool of knife-edge pixels (oracle scenes only)."""
+    bad = pixel_errors(out, ref, atol)
+    if exempt is not None:
+        bad &= ~exempt
     if bad.any():
-        errs.append(f"depth: {int(bad.sum())} px over tol, max err {max_err(d_out, d_ref):.3g}")
-    return errs
+        ys, xs = np.nonzero(bad)
+        return [f"{int(bad.sum())} px out of tolerance (first at y={ys[0]}, x={xs[0]}); max errs image "
+                f"{max_err(out['image'], ref['image']):.3g}, alpha {max_err(out['alpha'], ref['alpha']):.3g}, "
+                f"depth {max_err(out['depth'], ref['depth']):.3g}"]
+    return []
 
 
 def check_projection(out, ref, atol=IMG_ATOL):

@@ -59,16 +59,27 @@ def test_bad_arguments_are_reported(pkg):
     alt = C.c_int32(0)
     assert lib.gs_radix_sort_pairs(None, None, None, None, 10, 0, 40, 0, None, 0, C.byref(alt), None) == 1
     a = N.GsProjectArgs()
-    a.cam.tile_size = 32
     a.cam.image_width = a.cam.image_height = 8
-    assert lib.gs_project_forward(C.byref(a), None) == 3  # unsupported tile size
+    for bad in (0, -4, 257):  # tile_size outside [1, GS_MAX_TILE]
+        a.cam.tile_size = bad
+        assert lib.gs_project_forward(C.byref(a), None) == 3
     with pytest.raises(RuntimeError, match="gs_status=3"):
         N.check(lib.gs_project_forward(C.byref(a), None), "gs_project_forward")
-    a.cam.tile_size = 16
-    a.cam.radius_max = 56.0  # rects could span 9 tiles per axis (GS_MAX_RADIUS)
+    a.cam.tile_size = 1
+    a.cam.image_width = 4097  # 4097 tiles per axis: more than the 12-bit tile coordinates
     assert lib.gs_project_forward(C.byref(a), None) == 3
-    assert b"radius_max" in lib.gs_last_error()
+    a.cam.image_width, a.cam.tile_size = 4096, 2
+    a.cam.radius_max = 256.0  # 2*256+1 px over 2-px tiles: 258 tiles wide > GS_MAX_RECT_TILES
+    assert lib.gs_project_forward(C.byref(a), None) == 3
+    assert b"GS_MAX_RECT_TILES" in lib.gs_last_error()
+    a.cam.radius_max = 254.0  # 256 tiles: accepted (n = 0, nothing to launch)
+    assert lib.gs_project_forward(C.byref(a), None) == 0
+    a.cam.image_width = 300  # 150 tiles in x: any radius fits
+    a.cam.radius_max = 1e6
+    assert lib.gs_project_forward(C.byref(a), None) == 0
     a.cam.radius_max = float("nan")
+    assert lib.gs_project_forward(C.byref(a), None) == 3
+    a.cam.radius_max, a.cam.radius_min = 1.0, 2.0
     assert lib.gs_project_forward(C.byref(a), None) == 3
 
 
@@ -90,3 +101,5 @@ def test_workspace_queries(pkg):
     lib = pkg._native.load()
     assert lib.gs_radix_sort_workspace_bytes(4096 * 3) >= 4 * (256 * 3 + 256)
     assert lib.gs_bin_workspace_bytes(1) >= 4
+    # 8x8 cells per tile: ceil(L/8)^2 (the liveness bitmap and partial layouts)
+    assert [lib.gs_tile_quads(t) for t in (1, 8, 9, 12, 16, 24, 32, 256, 0, 257)] == [1, 1, 4, 4, 4, 9, 16, 1024, 0, 0]

@@ -46,9 +46,19 @@ def test_no_cpu_fallback(pkg):
         pkg.GaussianRenderer().render(_Cam(), m, pkg.RenderSettings(8, 8, torch.zeros(3)))
 
 
-def test_tile_size_must_be_16(pkg):
-    with pytest.raises(ValueError):
-        pkg.GaussianRenderer(tile_size=8)
+def test_renderer_constructor_range(pkg):
+    """GaussianRenderer(tile_size, radius_min, radius_max) (renderer.py:24-28):
+    any tile edge in [1, 256] and finite radii are taken as given."""
+    for t in (1, 8, 12, 16, 32, 256):
+        r = pkg.GaussianRenderer(tile_size=t, radius_max=80.0)
+        assert r.tile_size == t and r.radius_max == 80.0
+    c = pkg.camera_params(_Cam(), pkg.RenderSettings(20, 30, torch.zeros(3)), tile_size=8)
+    assert (c.tiles_x, c.tiles_y, c.cells) == (4, 3, 1)
+    assert pkg.camera_params(_Cam(), pkg.RenderSettings(20, 30, torch.zeros(3)), tile_size=32).cells == 16
+    for bad in (dict(tile_size=0), dict(tile_size=257), dict(tile_size=8.5), dict(radius_max=float("inf")),
+                dict(radius_min=3.0, radius_max=2.0)):
+        with pytest.raises(ValueError):
+            pkg.GaussianRenderer(**bad)
 
 
 def test_gaussian_model_layout(pkg):
