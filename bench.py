@@ -14,9 +14,12 @@ resident in HBM before the timed region.  `value` = all ranks' pixels /
 max-over-ranks step time.
 
 Also reported: the roofline of the dominant kernel (HIP events on the
-kernels' own stream, averaged over the timed steps) and a CPU baseline (the
-oracle, a C restatement of the reference path, on the host cores, rank 0,
-N=1 only).
+kernels' own stream, averaged over the timed steps), priced by SURVEY.md
+8(d)'s algorithmic byte and flop models from the frame's work counters
+(R, E, C, M), against the 8 TB/s spec and a copy kernel measured on the box;
+and a CPU baseline (the oracle, a C restatement of the reference path, on
+the host cores and on one core, rank 0, N=1 only) next to the literal
+reference's cost model.
 """
 from __future__ import annotations
 
@@ -35,6 +38,13 @@ sys.path.insert(0, ROOT)
 METRIC = "rendered Mpix/s fwd+bwd @1080p, 1M Gaussians; PSNR vs ref; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TFLOPS = 157.3     # FP32 vector, spec (FMA = 2)
+# literal reference cost model (measured on the survey
+# host): forward per evaluated pair (sparse / contributing), binning per
+# Gaussian, projection + cull + sort at 1M; backward per contributing pair
+# 155 ms at 256^2, O(H W) per pair (autograd CopySlices)
+REF_FWD_S_PER_PAIR, REF_FWD_S_PER_CONTRIB = 85e-6, 177e-6
+REF_BIN_S_PER_GAUSSIAN, REF_PROJ_SORT_S_PER_1M = 8.7e-6, 0.40
+REF_BWD_S_PER_CONTRIB_PX = 155e-3 / (256 * 256)
 
 
 def parse():
@@ -48,7 +58,8 @@ def parse():
     ap.add_argument("--no-optimizer", action="store_true", help="time render fwd+bwd only")
     ap.add_argument("--diag-steps", type=int, default=5, help="untimed steps for the per-stage breakdown")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="oracle threads (capped by the CPUs this process may run on); the box's share is 16")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI) for the driver; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--force-dist", action="store_true",
@@ -77,17 +88,38 @@ class BenchCamera:
         return self._wv
 
 
-def algorithmic_counts(fr, H, W, tiles_x, tiles_y):
-    """R (records consumed per tile: list prefix up to the deepest pixel's
-    last evaluated entry), E (evaluated pairs), from the forward's saved
-    per-pixel state."""
+def algorithmic_counts(fr, pair_counts, H, W, tiles_x, tiles_y):
+    """SURVEY 8(d) work counters of one frame: R (records consumed per tile:
+    list prefix up to the deepest pixel's last evaluated entry), E (evaluated
+    pairs) from the forward's saved per-pixel state, C (contributing pairs)
+    from the forward's measurement counter."""
     neval = fr.pix_state[:, 1].contiguous().view(torch.int32).view(H, W).to(torch.int64)
     E = int(neval.sum())
     pad = torch.zeros(tiles_y * 16, tiles_x * 16, dtype=torch.int64, device=neval.device)
     pad[:H, :W] = neval
     per_tile = pad.view(tiles_y, 16, tiles_x, 16).amax(dim=(1, 3))
     R = int(per_tile.sum())
-    return R, E
+    C = int(pair_counts.to(torch.int64).sum())
+    return R, E, C
+
+
+def copy_peak_gbs(dev, nbytes=1 << 30, reps=10):
+    """HBM bandwidth a plain device copy reaches on this box (read + write
+    bytes / time, 1 GiB buffers, HIP events): the achievable peak beside the
+    8 TB/s spec (the guide measured ~6.3 TB/s with a float4 copy)."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    e1.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return gbs
 
 
 def main():
@@ -196,36 +228,52 @@ def main():
         # re-run the forward pipeline to read its frame state (not timed)
         from mini3dgs_amd import rasterizer as RZ
         camp = pkg.camera_params(cam, settings)
+        pair_counts = torch.empty((H * W,), dtype=torch.int32, device=dev)
         _, _, _, _, _, _, _, fr = RZ.forward_pipeline(
             camp, model._xyz, None, model._scaling, model._rotation, model._features_dc[:, 0, :],
-            torch.sigmoid(model._opacity).squeeze(1))
-        R, E = algorithmic_counts(fr, H, W, tiles_x, tiles_y)
+            torch.sigmoid(model._opacity).squeeze(1), pair_counts=pair_counts)
+        R, E, Cc = algorithmic_counts(fr, pair_counts, H, W, tiles_x, tiles_y)
         M, T = fr.M, fr.T
         num_tiles = tiles_x * tiles_y
-        # algorithmic bytes per launch
-        bytes_fwd = 44 * R + 8 * num_tiles + 20 * H * W + 24 * H * W
-        bytes_bwd = 44 * R + 4 * R + 40 * R + 8 * num_tiles + (24 + 20) * H * W
-        # algorithmic fp32 flops per evaluated pair:
-        # forward 26 (s, exp, alpha, composite); backward 66 (replay 26,
-        # alpha / colour / depth gradient 20, the 10 per-pair sums 20)
-        flops_fwd, flops_bwd = 26 * E, 66 * E
+        # SURVEY 8(d) algorithmic bytes per launch: the consumed records (44 B:
+        # mean 8, conic 12, opacity 4, colour 12, depth 4, gradient slot 4),
+        # tile ranges, per-pixel outputs + saved state (20 + 8 B) forward;
+        # records, per-pixel state + cotangents (36 B) and 40 B of gradient per
+        # visible Gaussian backward
+        bytes_fwd = 44 * R + 8 * num_tiles + 28 * H * W
+        bytes_bwd = 44 * R + 36 * H * W + 40 * M
+        # SURVEY 8(d) flops: forward 26 per evaluated pair; backward 70 per
+        # contributing pair + 12 per other visited (evaluated) pair
+        flops_fwd, flops_bwd = 26 * E, 70 * Cc + 12 * (E - Cc)
         kern = {"blend_fwd": (bytes_fwd, flops_fwd), "blend_bwd": (bytes_bwd, flops_bwd)}
         dom = max((k for k in kern if k in stages), key=lambda k: stages[k]) if stages else "blend_bwd"
         # the dominant kernel's average launch, measured live in the timed region
         t_ms = sum(bwd_live) / len(bwd_live) if dom == "blend_bwd" and bwd_live else stages[dom]
         ach = kern[dom][0] / (t_ms * 1e-3) / 1e9
+        copy_gbs = copy_peak_gbs(dev)
         traffic, tnote = pmc_traffic(dom)
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tnote,
-                "avg_launch_ms": round(t_ms, 4), "algorithmic_bytes_per_launch": int(kern[dom][0])}
-        if kern[dom][1]:
-            tf = kern[dom][1] / (t_ms * 1e-3) / 1e12
-            roof["valu"] = {"achieved_tflops": round(tf, 2), "peak_tflops": VALU_PEAK_TFLOPS,
-                            "frac": round(tf / VALU_PEAK_TFLOPS, 4)}
+                "avg_launch_ms": round(t_ms, 4), "algorithmic_bytes_per_launch": int(kern[dom][0]),
+                "bytes_model": "44 R + 36 H W + 40 M (SURVEY 8d)" if dom == "blend_bwd"
+                else "44 R + 8 tiles + 28 H W (SURVEY 8d)",
+                "measured_copy_peak": round(copy_gbs, 1), "frac_of_measured_copy": round(ach / copy_gbs, 4)}
+        tf = kern[dom][1] / (t_ms * 1e-3) / 1e12
+        roof["valu"] = {"achieved_tflops": round(tf, 2), "peak_tflops": VALU_PEAK_TFLOPS,
+                        "frac": round(tf / VALU_PEAK_TFLOPS, 4),
+                        "flops_model": "70 C + 12 (E - C) (SURVEY 8d)" if dom == "blend_bwd" else "26 E (SURVEY 8d)"}
+        # the other blend kernel, same models (its time from the diagnostic steps)
+        other = "blend_fwd" if dom == "blend_bwd" else "blend_bwd"
+        if other in stages:
+            to = stages[other]
+            roof["other_blend"] = {"kernel": other, "avg_ms": round(to, 4),
+                                   "hbm_frac": round(kern[other][0] / (to * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "valu_frac": round(kern[other][1] / (to * 1e-3) / 1e12 / VALU_PEAK_TFLOPS, 4)}
         # --- CPU baseline ---------------------------------------------------
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(scene, W, H, cot, a.cpu_threads)
+            cpu["reference_cost_model"] = reference_cost_model(H, W, M, E, Cc)
         line = {
             "metric": METRIC, "value": round(mpix, 3), "unit": "Mpix/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
@@ -234,7 +282,7 @@ def main():
                                    "render fwd+bwd" + ("" if opt is None else " + grad all-reduce + Adam step"),
                        "gaussians": n, "width": W, "height": H, "views_per_step": world,
                        "parallelism": f"dp{world} (one view per GPU)", "visible": M, "tile_touches": T,
-                       "records_consumed": R, "evaluated_pairs": E},
+                       "records_consumed": R, "evaluated_pairs": E, "contributing_pairs": Cc},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
             "stages_note": f"HIP-event intervals from {a.diag_steps} diagnostic steps after the timed region "
                            "(each interval also holds any host launch gap before its kernels; kernel-only "
@@ -250,10 +298,9 @@ def main():
 
 def pmc_traffic(stage):
     """HBM bytes per launch of the stage's kernel from the committed PMC
-    summary of this build (tools/pmc.sh -> profiles/pmc_current.txt):
-    (FETCH_SIZE + WRITE_SIZE) x 1 KiB.  Raw: the guide's x2 FETCH_SIZE
-    correction is calibrated for 16-B/lane streaming reads only, and these
-    kernels gather 48-B records (MI355X_MICROARCH.md, HBM)."""
+    summary of this build (tools/pmc.sh -> profiles/pmc_current.txt), as
+    MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE doubled (gfx950
+    tallies 128-B read requests at 64 B) + WRITE_SIZE, KiB -> bytes."""
     path = os.path.join(ROOT, "profiles", "pmc_current.txt")
     if not os.path.exists(path):
         return None, None
@@ -267,15 +314,19 @@ def pmc_traffic(stage):
                 vals[parts[0]] = float(parts[1])
     if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
         return None, None
-    return int((vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), \
-        "profiles/pmc_current.txt (rocprofv3 --pmc FETCH_SIZE + WRITE_SIZE, KiB, uncorrected)"
+    return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), \
+        (f"profiles/pmc_current.txt: 2 x FETCH_SIZE ({vals['FETCH_SIZE'] * 1024 / 1e6:.1f} MB raw) + WRITE_SIZE "
+         f"({vals['WRITE_SIZE'] * 1024 / 1e6:.1f} MB), rocprofv3 --pmc, one pass each")
 
 
 def cpu_baseline(scene, W, H, cot, threads):
     """Oracle (C restatement of the reference render path) fwd+bwd on the
-    host cores for the same C3 frame; bounded: one frame."""
+    host cores for the same C3 frame, then on one core; bounded: one frame
+    each (~1 s and ~15 s)."""
     import numpy as np
     from oracle import oracle as orc  # CPU baseline leg: test infrastructure only
+    avail = len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, avail))
     cov = orc.covariance(scene.scaling.numpy(), scene.rotation.numpy())
     s = orc.Scene(xyz=scene.xyz.numpy(), cov3d=cov, color_logits=scene.features_dc[:, 0].numpy(),
                   opacity=torch.sigmoid(scene.opacity[:, 0]).numpy(), wv=np.eye(4), width=W, height=H,
@@ -284,9 +335,27 @@ def cpu_baseline(scene, W, H, cot, threads):
     t0 = time.perf_counter()
     orc.render_backward(s, gi, ga, gd, nthreads=threads)
     dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    orc.render_backward(s, gi, ga, gd, nthreads=1)
+    dt1 = time.perf_counter() - t0
     return {"value": round(H * W / dt / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
             "sample": f"one full C3 frame ({W}x{H}, {scene.xyz.shape[0]} Gaussians) fwd+bwd, "
-                      f"oracle/gs_oracle.c with OpenMP x{threads}, {dt:.2f} s"}
+                      f"oracle/gs_oracle.c with OpenMP x{threads} ({dt:.2f} s) and on 1 core ({dt1:.2f} s)",
+            "one_core": {"value": round(H * W / dt1 / 1e6, 4), "unit": "Mpix/s", "cores": 1},
+            "host_cpus_schedulable": avail}
+
+
+def reference_cost_model(H, W, M, E, C):
+    """The literal reference (Python per-pixel loop + autograd) priced by
+    BASELINE.md section 2's measured coefficients and this frame's counters
+    (M visible, E evaluated, C contributing pairs)."""
+    fwd = (REF_FWD_S_PER_PAIR * (E - C) + REF_FWD_S_PER_CONTRIB * C + REF_BIN_S_PER_GAUSSIAN * M
+           + REF_PROJ_SORT_S_PER_1M * M / 1e6)
+    bwd = REF_BWD_S_PER_CONTRIB_PX * H * W * C
+    return {"fwd_hours": round(fwd / 3600, 1), "bwd_hours": round(bwd / 3600, 1),
+            "value": H * W / (fwd + bwd) / 1e6, "unit": "Mpix/s", "cores": 1,
+            "note": "BASELINE.md section 2 coefficients x this frame's E, C, M (not run: the reference "
+                    "cannot travel to the GPU box)"}
 
 
 if __name__ == "__main__":

@@ -203,6 +203,8 @@ typedef struct gs_blend_fwd_args {
   float *pix_state;             /* [H*W,2] */
   uint64_t *live_bits;          /* [gs_tile_quads(tile_size), live_words]: see gs_blend_live_words */
   int64_t live_words;
+  uint32_t *pair_counts;        /* [H*W] or NULL: each pixel's contributing pairs (c > 0), the
+                                   work counter C of SURVEY 8(d); measurement only */
 } gs_blend_fwd_args;
 gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
 

@@ -78,6 +78,7 @@ class GsBlendFwdArgs(C.Structure):
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
         ("sorted_gauss", _vp), ("records", _vp), ("image", _vp), ("alpha", _vp), ("depth", _vp),
         ("pix_acc", _vp), ("pix_state", _vp), ("live_bits", _vp), ("live_words", C.c_int64),
+        ("pair_counts", _vp),
     ]
 
 

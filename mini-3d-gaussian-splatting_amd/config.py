@@ -4,8 +4,12 @@ are the reference's; the few the trainer adds are marked."""
 from __future__ import annotations
 
 from dataclasses import asdict, dataclass, fields
+from pathlib import Path
 
-import yaml
+try:  # optional, as in the reference (config.py:1-8)
+    import yaml
+except ImportError:  # pragma: no cover
+    yaml = None
 
 
 @dataclass
@@ -48,13 +52,20 @@ class TrainingConfig:
     sh_increase_interval: int = 1000   # active SH degree +1 every this many iterations, up to sh_degree
 
 
+def _need_yaml():
+    if yaml is None:
+        raise ImportError("PyYAML is not installed")
+
+
 class ConfigManager:
     """config.py:69-95: YAML load / save of the flat config (unknown keys are
-    rejected instead of silently ignored)."""
+    rejected instead of silently ignored).  The reference's names
+    (load_from_yaml, save_to_yaml, get_default_config) and short aliases."""
 
     @staticmethod
-    def load(path: str) -> TrainingConfig:
-        with open(path) as f:
+    def load_from_yaml(config_path: str) -> TrainingConfig:
+        _need_yaml()
+        with open(config_path, encoding="utf-8") as f:
             data = yaml.safe_load(f) or {}
         names = {f.name for f in fields(TrainingConfig)}
         unknown = sorted(set(data) - names)
@@ -63,6 +74,15 @@ class ConfigManager:
         return TrainingConfig(**data)
 
     @staticmethod
-    def save(cfg: TrainingConfig, path: str) -> None:
-        with open(path, "w") as f:
-            yaml.safe_dump(asdict(cfg), f, sort_keys=False)
+    def save_to_yaml(config: TrainingConfig, config_path: str) -> None:
+        _need_yaml()
+        Path(config_path).parent.mkdir(parents=True, exist_ok=True)
+        with open(config_path, "w", encoding="utf-8") as f:
+            yaml.safe_dump(asdict(config), f, sort_keys=False, allow_unicode=True)
+
+    @staticmethod
+    def get_default_config() -> TrainingConfig:
+        return TrainingConfig()
+
+    load = load_from_yaml
+    save = save_to_yaml

@@ -793,9 +793,14 @@ __device__ __forceinline__ float2 lds_pair(const float2 *p) {
   return make_float2(__uint_as_float((uint32_t)v), __uint_as_float((uint32_t)(v >> 32)));
 }
 
+// kCount: also count each pixel's contributing pairs (c > 0) into
+// a.pair_counts -- a work counter for the measurement, off in the
+// render path.
+// kT16: tile_size is the default 16 (its cell geometry folds to constants).
+template <bool kCount, bool kT16>
 __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
   __shared__ float2 s_rec[kBlock * 6];
-  const CellGeom cg(a.cam.tile_size);
+  const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
   const int ng = cg.groups();
   const int tile = (int)blockIdx.x / ng, grp = (int)blockIdx.x - tile * ng;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -817,7 +822,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
   // image start done.  No loop-carried bool: "done" is one compare, not a
   // mask in SGPRs.
   float A = inside ? 0.f : 1.f, D = 0.f;
-  uint32_t neval = 0;
+  uint32_t neval = 0, ncontrib = 0;
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   __shared__ uint32_t s_live[4];
@@ -902,6 +907,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
           ab = __builtin_fmaf(c, pbz.x, ab);
           A = A + c;
           D = __builtin_fmaf(c, pbz.y, D);
+          if constexpr (kCount) ncontrib += c > 0.f ? 1u : 0u;
           // :352 (after accumulation): the terminating entry is the last one
           // reached while the pixel still ran (A only grows; a pixel still
           // running at the end of its list gets end - start below)
@@ -932,6 +938,7 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
   a.depth[p] = D / (A + 1e-6f);  // :362
   reinterpret_cast<float4 *>(a.pix_acc)[p] = make_float4(ar, ag, ab, D);
   reinterpret_cast<float2 *>(a.pix_state)[p] = make_float2(A, __uint_as_float(neval));
+  if constexpr (kCount) a.pair_counts[p] = ncontrib;
 }
 
 // ======================================================== blend bwd =======
@@ -1012,11 +1019,12 @@ __device__ __forceinline__ void quad_tile(int ncell, int &tile, int &quad) {
   tile = (int)((grp / q) * 8u + (b & 7u));
 }
 
+template <bool kT16>
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
   __shared__ float2 s_wrec[kWave * 6];   // the word's live records, packed in bit order; word 10 = slot
-  const CellGeom cg(a.cam.tile_size);
+  const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
   const int ncell = cg.cells();
   int tile, quad;
   quad_tile(ncell, tile, quad);
@@ -1282,6 +1290,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
 // together, and consecutive Gaussians' slots are adjacent (index-order
 // slots): coalesced.  Flags of up to 4 slots are loaded at once, then their
 // partials: two round trips per 8 slots of g (the mean is 4.4 on C3).
+template <bool kT16>
 __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) {
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const int g = (int)(t >> 3), h = (int)((t >> 2) & 1), q = (int)(t & 3);
@@ -1301,7 +1310,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
   asm volatile("" : "+v"(off32));
   const uint32_t cnt = (valid && visb) ? rect_touches(tx0, tx1, ty0, ty1) : 0u;
   // lane q sums cells q, q + 4, ... of the tile's Q (one pass when Q = 4)
-  const uint32_t ncell = (uint32_t)CellGeom(a.cam.tile_size).cells();
+  const uint32_t ncell = (uint32_t)CellGeom(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size).cells();
   for (uint32_t qc = (uint32_t)q; cnt > (uint32_t)h && qc < ncell; qc += 4) {
     const size_t off = off32;
     const uint8_t *flag = a.slot_live + off * ncell + qc;  // (slot e, cell qc) at flag[Q e]
@@ -1832,7 +1841,13 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   const long long blocks = (long long)a->tiles_x * a->tiles_y * gx * gx;
   if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_forward");
   if (blocks == 0) return GS_OK;
-  k_blend_fwd<<<(unsigned)blocks, kBlock, 0, s>>>(*a);
+  const bool t16 = a->cam.tile_size == GS_DEFAULT_TILE;
+  if (a->pair_counts)
+    k_blend_fwd<true, false><<<(unsigned)blocks, kBlock, 0, s>>>(*a);
+  else if (t16)
+    k_blend_fwd<false, true><<<(unsigned)blocks, kBlock, 0, s>>>(*a);
+  else
+    k_blend_fwd<false, false><<<(unsigned)blocks, kBlock, 0, s>>>(*a);
   return check_launch("gs_blend_forward");
 }
 
@@ -1849,7 +1864,10 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (num_tiles <= 0) return GS_OK;
   const long long blocks = (long long)div_up(num_tiles, 8) * 8LL * cells_per_tile(a->cam.tile_size);
   if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_backward");
-  k_blend_bwd<<<(unsigned)blocks, kWave, 0, s>>>(*a);
+  if (a->cam.tile_size == GS_DEFAULT_TILE)
+    k_blend_bwd<true><<<(unsigned)blocks, kWave, 0, s>>>(*a);
+  else
+    k_blend_bwd<false><<<(unsigned)blocks, kWave, 0, s>>>(*a);
   return check_launch("gs_blend_backward");
 }
 
@@ -1867,7 +1885,12 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
                 "gs_project_backward");
   if (a->pair_grads && !cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
-  if (a->pair_grads) k_gather_slots<<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  if (a->pair_grads) {
+    if (a->cam.tile_size == GS_DEFAULT_TILE)
+      k_gather_slots<true><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
+    else
+      k_gather_slots<false><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
+  }
   const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
   if (hot)
     k_project_bwd<true><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);

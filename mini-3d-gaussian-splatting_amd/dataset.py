@@ -195,6 +195,50 @@ class COLMAPDataset(CameraDataset):
         return str(self._sparse() / "points3D.txt")
 
 
+def load_point_cloud(path: str):
+    """(points [N,3] f32, colours [N,3] f32 in [0,1] or None) from the formats
+    the reference's IOUtils.load_point_cloud reads (io_utils.py:34-83): .npz
+    (points / colors, no pickles), .npy ([N,3] or [N,>=6]), COLMAP
+    points3D.txt, or text lines "x y z [r g b]"."""
+    p = Path(path)
+    suf = p.suffix.lower()
+    if suf == ".npz":
+        with np.load(str(p), allow_pickle=False) as z:
+            pts = z["points"] if "points" in z.files else np.zeros((0, 3), np.float32)
+            cols = z["colors"] if "colors" in z.files else None
+        return pts.astype(np.float32).reshape(-1, 3), None if cols is None else cols.astype(np.float32).reshape(-1, 3)
+    if suf == ".npy":
+        arr = np.load(str(p), allow_pickle=False)
+        if arr.ndim == 2 and arr.shape[1] >= 6:
+            return arr[:, :3].astype(np.float32), arr[:, 3:6].astype(np.float32)
+        return arr[:, :3].astype(np.float32), None
+    pts, cols = [], []
+    colmap = p.name == "points3D.txt"
+    with open(p, encoding="utf-8", errors="ignore") as f:
+        for line in f:
+            line = line.strip()
+            if not line or line.startswith("#"):
+                continue
+            el = line.split()
+            if colmap:
+                if len(el) < 10:
+                    continue
+                pts.append([float(v) for v in el[1:4]])
+                cols.append([float(v) / 255.0 for v in el[4:7]])
+            else:
+                try:
+                    v = [float(x) for x in el]
+                except ValueError:
+                    continue
+                if len(v) >= 3:
+                    pts.append(v[:3])
+                    if len(v) >= 6:
+                        cols.append(v[3:6])
+    P = np.asarray(pts, np.float32).reshape(-1, 3)
+    Cc = np.asarray(cols, np.float32).reshape(-1, 3) if cols and len(cols) == len(pts) else None
+    return P, Cc
+
+
 def load_dataset(path: str, white_background: bool = False, device=None) -> CameraDataset:
     """NeRF-synthetic if transforms_train.json exists, else COLMAP."""
     p = Path(path)
@@ -204,4 +248,4 @@ def load_dataset(path: str, white_background: bool = False, device=None) -> Came
     return ds
 
 
-__all__ = ["CameraDataset", "NeRFSyntheticDataset", "COLMAPDataset", "load_dataset"]
+__all__ = ["CameraDataset", "NeRFSyntheticDataset", "COLMAPDataset", "load_dataset", "load_point_cloud"]

@@ -34,7 +34,10 @@ class GradAllReduce:
         self.params: List[torch.nn.Parameter] = list(params)
         self._flat: Optional[torch.Tensor] = None
         self._sizes: List[int] = []
-        self._avg: Optional[bool] = None  # ReduceOp.AVG usable (nccl = RCCL); decided on first use
+        # RCCL (backend "nccl") forms the mean inside the reduction (ReduceOp.AVG,
+        # NCCL >= 2.10); gloo has no AVG: SUM, then one division.  Decided once.
+        self._avg: bool = (dist.is_initialized() and dist.get_backend(group) == "nccl"
+                           and hasattr(dist.ReduceOp, "AVG")) if hasattr(dist, "is_initialized") else False
 
     def _bucket(self) -> torch.Tensor:
         sizes = [p.numel() for p in self.params]
@@ -80,17 +83,12 @@ class GradAllReduce:
             else:
                 v.copy_(p.grad.reshape(-1))
         world = self.dist.get_world_size(self.group)
-        if self._avg is None:
-            self._avg = self.dist.get_backend(self.group) == "nccl" and hasattr(self.dist.ReduceOp, "AVG")
         if self._avg:
             # RCCL divides inside the reduction: no extra pass over the bucket
-            try:
-                self.dist.all_reduce(flat, op=self.dist.ReduceOp.AVG, group=self.group)
-                return self._copy_out(views, in_place)
-            except (RuntimeError, ValueError):
-                self._avg = False  # a build without AVG: sum, then divide (the bucket is unchanged)
-        self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
-        flat.div_(world)
+            self.dist.all_reduce(flat, op=self.dist.ReduceOp.AVG, group=self.group)
+        else:
+            self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
+            flat.div_(world)
         self._copy_out(views, in_place)
 
     def _copy_out(self, views, in_place) -> None:

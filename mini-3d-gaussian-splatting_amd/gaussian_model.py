@@ -109,6 +109,20 @@ class GaussianModel(nn.Module):
                   torch.full((n, 3), math.log(base), device=dev),
                   F.normalize(torch.randn(n, 4, device=dev), dim=-1), torch.full((n, 1), 0.5, device=dev))
 
+    @torch.no_grad()
+    def create_from_pcd(self, pcd_path: str, spatial_lr_scale: float = 1.0, device=None) -> None:
+        """gaussian_model.py:42-76: initialise from a point-cloud file (the
+        formats of dataset.load_point_cloud; the reference's own loader call,
+        IOUtils.load_pcd, does not exist)."""
+        from .dataset import load_point_cloud
+        pts, cols = load_point_cloud(pcd_path)
+        if pts.shape[0] == 0:
+            raise ValueError("No points found in the PCD file.")
+        dev = torch.device(device) if device is not None else (
+            torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+        self.create_from_points(torch.from_numpy(pts).to(dev),
+                                None if cols is None else torch.from_numpy(cols).to(dev), spatial_lr_scale)
+
     # -- accessors (gaussian_model.py:101-128) ------------------------------
     @property
     def get_xyz(self) -> torch.Tensor:
@@ -165,6 +179,11 @@ class GaussianModel(nn.Module):
     def parameter_list(self):
         """The six parameters in gs_model_arrays order."""
         return [self._xyz, self._features_dc, self._features_rest, self._scaling, self._rotation, self._opacity]
+
+    def get_parameters(self):
+        """The parameter list the reference's optimizer asks for
+        (optimizer.py:71, `gaussians.get_parameters()`)."""
+        return self.parameter_list()
 
     # -- densification (gaussian_model.py:130-197, optimizer.py:34-67) --------
     @torch.no_grad()

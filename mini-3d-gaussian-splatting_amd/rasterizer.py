@@ -163,7 +163,9 @@ def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cells: int, dev):
 
 
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
-                     sh_rest=None, sh_degree=0):
+                     sh_rest=None, sh_degree=0, pair_counts=None):
+    """pair_counts: optional int32 [H*W] the blend fills with each pixel's
+    contributing pairs (a measurement counter; not in render())."""
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -279,7 +281,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
 
     fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), p_tv[alt.value], N.ptr(records),
                           N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state),
-                          p_live, live_words)
+                          p_live, live_words, N.ptr(pair_counts))
     StageTimer.mark("blend_fwd")
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
     StageTimer.mark("~end_fwd")

@@ -47,15 +47,28 @@ class GaussianTrainer:
         self._perm: Optional[np.ndarray] = None
 
     # -- setup (trainer.py:32-44) ------------------------------------------
-    def setup(self) -> None:
+    def _device(self) -> torch.device:
         c = self.config
-        dev = torch.device(c.device if c.device != "cuda" else f"cuda:{torch.cuda.current_device()}")
+        return torch.device(c.device if c.device != "cuda" else f"cuda:{torch.cuda.current_device()}")
+
+    def _setup_run(self) -> None:
+        """Everything but the model: dataset, process group, scene extent and
+        the camera order -- shared by setup() and load_checkpoint() (a resumed
+        run needs them as much as a fresh one)."""
+        c = self.config
         if self.dataset is None:
-            self.dataset = load_dataset(c.data_path, device=dev)
+            self.dataset = load_dataset(c.data_path, device=self._device())
         if torch.distributed.is_available() and torch.distributed.is_initialized() and \
                 torch.distributed.get_world_size() > 1:
             self._dist = torch.distributed
         self.scene_extent = self.get_scene_extent()
+        n = len(self.dataset.get_train_cameras())
+        self._perm = np.random.default_rng(c.seed).permutation(n)
+
+    def setup(self) -> None:
+        c = self.config
+        dev = self._device()
+        self._setup_run()
         g = GaussianModel(c)
         gen = torch.Generator().manual_seed(c.seed)
         if self.dataset.points is not None and len(self.dataset.points):
@@ -67,8 +80,6 @@ class GaussianTrainer:
         self.gaussians = g
         self.optimizer = GaussianOptimizer(g, c)
         self.optimizer.setup_optimizer()
-        n = len(self.dataset.get_train_cameras())
-        self._perm = np.random.default_rng(c.seed).permutation(n)
 
     def get_scene_extent(self) -> float:
         """trainer.py:87-89: camera-centre radius (get_scene_info)."""
@@ -115,6 +126,8 @@ class GaussianTrainer:
     def train(self, iterations: Optional[int] = None) -> None:
         if self.gaussians is None:
             self.setup()
+        elif self._perm is None:
+            self._setup_run()
         n = self.config.iterations if iterations is None else iterations
         for _ in range(n):
             self.iteration += 1
@@ -178,6 +191,9 @@ class GaussianTrainer:
                                                      "exp_avg_sq": t[f"adam.{name}.v"].to(dev)}
         self.iteration = int(meta.get("iteration", iteration))
         self.gaussians.active_sh_degree = int(meta.get("active_sh_degree", 0))
+        self._reducer = None
+        if self._perm is None:
+            self._setup_run()
 
 
 __all__ = ["GaussianTrainer", "TrainingConfig"]

@@ -102,3 +102,31 @@ def test_lr_schedule(pkg):
     dc = pkg.optim.DensityController(pkg.TrainingConfig())
     assert dc.should_densify(500) and dc.should_densify(15000) and not dc.should_densify(550)
     assert not dc.should_densify(400) and not dc.should_densify(15100)
+
+
+def test_reference_api_names(pkg, tmp_path):
+    """Reference entry points kept under their names: ConfigManager
+    load_from_yaml / save_to_yaml / get_default_config (config.py:69-95),
+    GaussianModel.create_from_pcd (gaussian_model.py:42-76) over the point
+    formats of IOUtils.load_point_cloud (io_utils.py:34-83), get_parameters."""
+    import numpy as np
+    cm = pkg.ConfigManager
+    cfg = cm.get_default_config()
+    cfg.iterations = 123
+    cm.save_to_yaml(cfg, str(tmp_path / "sub" / "c.yaml"))
+    assert cm.load_from_yaml(str(tmp_path / "sub" / "c.yaml")).iterations == 123
+    pts = np.array([[0, 0, 0], [1, 2, 3], [-1, 0.5, 2]], np.float32)
+    cols = np.array([[1, 0, 0], [0, 1, 0], [0, 0, 1]], np.float32)
+    np.savez(tmp_path / "p.npz", points=pts, colors=cols)
+    np.save(tmp_path / "p.npy", np.concatenate([pts, cols], 1))
+    (tmp_path / "p.txt").write_text("".join(" ".join(map(str, r)) + "\n" for r in pts))
+    (tmp_path / "points3D.txt").write_text("# id x y z r g b err track\n" + "".join(
+        f"{i} {p[0]} {p[1]} {p[2]} {int(c[0] * 255)} {int(c[1] * 255)} {int(c[2] * 255)} 0.1 1 2\n"
+        for i, (p, c) in enumerate(zip(pts, cols))))
+    for name, has_col in (("p.npz", True), ("p.npy", True), ("p.txt", False), ("points3D.txt", True)):
+        m = pkg.GaussianModel()
+        m.create_from_pcd(str(tmp_path / name), device="cpu")
+        assert torch.allclose(m._xyz, torch.from_numpy(pts)), name
+        want = torch.from_numpy(cols) if has_col else torch.ones(3, 3)
+        assert torch.allclose(m._features_dc[:, 0], want), name
+        assert len(m.get_parameters()) == 6

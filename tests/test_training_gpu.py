@@ -68,3 +68,11 @@ def test_trainer_learns_and_checkpoints(pkg, cuda, tmp_path):
         assert torch.equal(a.detach(), b.detach())
     assert tr2.iteration == tr.iteration and path.endswith(".safetensors")
     assert math.isclose(tr2.validate()["psnr"], after["psnr"], rel_tol=1e-6)
+    # resuming trains on: the run state (cameras, scene extent) is rebuilt by
+    # load_checkpoint, and the resumed run takes the same steps as the original
+    assert tr2.scene_extent == tr.scene_extent and tr2._perm is not None
+    tr.train(5)
+    tr2.train(5)
+    assert tr2.iteration == tr.iteration
+    for a, b in zip(tr.gaussians.parameter_list(), tr2.gaussians.parameter_list()):
+        assert torch.equal(a.detach(), b.detach())
