@@ -4,46 +4,19 @@ available offline; BASELINE config C4 names the lego scene), then
 GaussianTrainer (render -> fused L1+D-SSIM -> backward -> FusedAdam ->
 densify) from a random init.  Checks the PSNR rises and checkpoints
 round-trip."""
-import json
 import math
 
-import numpy as np
 import pytest
 import torch
 
-from test_training_cpu import look_at_c2w_gl, _png
+from scene_util import load_scene, write_scene_files
 
 pytestmark = pytest.mark.gpu
 
 
 def _scene(pkg, tmp_path, cuda, n_views=12, size=64):
-    (tmp_path / "train").mkdir()
-    frames = []
-    rng = np.random.default_rng(0)
-    for i in range(n_views):
-        th, ph = 2 * math.pi * i / n_views, 0.3 + 0.4 * rng.random()
-        C = 4.0 * np.array([math.cos(th) * math.cos(ph), math.sin(th) * math.cos(ph), math.sin(ph)])
-        _png(tmp_path / "train" / f"r_{i}.png", size, size, np.zeros((size, size, 4), np.uint8))
-        frames.append({"file_path": f"./train/r_{i}", "transform_matrix": look_at_c2w_gl(C).tolist()})
-    (tmp_path / "transforms_train.json").write_text(json.dumps({"camera_angle_x": 0.69, "frames": frames}))
-    ds = pkg.NeRFSyntheticDataset(str(tmp_path), device=cuda)
-    ds.load_cameras()
-    # ground truth: 1500 Gaussians in a ball of radius 0.7
-    g = torch.Generator().manual_seed(3)
-    n = 1500
-    d = torch.randn(n, 3, generator=g)
-    xyz = d / d.norm(dim=1, keepdim=True) * 0.7 * torch.rand(n, 1, generator=g) ** (1 / 3)
-    gt = pkg.GaussianModel()
-    gt._set(xyz.to(cuda), (torch.rand(n, 1, 3, generator=g) * 4 - 2).to(cuda), torch.zeros(n, 15, 3, device=cuda),
-            torch.log(0.03 + 0.05 * torch.rand(n, 3, generator=g)).to(cuda),
-            torch.nn.functional.normalize(torch.randn(n, 4, generator=g), dim=-1).to(cuda),
-            torch.full((n, 1), 1.5).to(cuda))
-    r = pkg.GaussianRenderer()
-    with torch.no_grad():
-        for cam in ds.get_train_cameras():
-            cam._image = r.render(cam, gt, pkg.RenderSettings(size, size, torch.zeros(3)))["image"].clone()
-    ds.split_train_test(0.25)
-    return ds
+    write_scene_files(tmp_path, n_views, size)
+    return load_scene(pkg, tmp_path, cuda, size)
 
 
 def test_trainer_learns_and_checkpoints(pkg, cuda, tmp_path):
