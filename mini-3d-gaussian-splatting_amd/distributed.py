@@ -4,14 +4,22 @@ SURVEY.md 8(e): each rank renders its own camera with a full replica of the
 GaussianModel; the only exchange per step is the mean of the Gaussian
 parameter gradients, done as ONE flat all_reduce(SUM) / world over
 torch.distributed (backend "nccl" = RCCL over xGMI on MI355X, "gloo" on CPU
-for tests), issued after the last backward kernel and before
-optimizer.step().  Payload: xyz 3 + features_dc 3 + scaling 3 + rotation 4 +
-opacity 1 = 14 fp32 (56 B) per Gaussian; features_rest has an identically
-zero render gradient and is not sent unless SH colour is on
-(GaussianModel.grad_parameters: +45 fp32 per Gaussian then).
+for tests), before optimizer.step().  Payload: xyz 3 + features_dc 3 +
+scaling 3 + rotation 4 + opacity 1 = 14 fp32 (56 B) per Gaussian;
+features_rest has an identically zero render gradient and is not sent unless
+SH colour is on (GaussianModel.grad_parameters: +45 fp32 per Gaussian then).
+
+Overlap: with the bucket attached (zero copy), the render backward runs its
+last stage (gradient gather + projection backward) in `chunks` ranges of
+Gaussians and hands each finished range to rows_ready(), which issues its
+all-reduces asynchronously (RCCL's own stream waits for the range's kernels
+only): range k's reduction runs while range k+1 is computed.
+all_reduce_mean() then waits for them.  Every rank issues the same ranges in
+the same order (same N, same chunk rule), as collectives must match.
 """
 from __future__ import annotations
 
+import os
 from typing import Iterable, List, Optional
 
 import torch
@@ -26,7 +34,8 @@ class GradAllReduce:
     take part in the collective.
     """
 
-    def __init__(self, params: Iterable[torch.nn.Parameter], dist=None, group=None):
+    def __init__(self, params: Iterable[torch.nn.Parameter], dist=None, group=None, chunks: Optional[int] = None,
+                 min_chunk_rows: Optional[int] = None):
         if dist is None:
             import torch.distributed as dist
         self.dist = dist
@@ -34,6 +43,13 @@ class GradAllReduce:
         self.params: List[torch.nn.Parameter] = list(params)
         self._flat: Optional[torch.Tensor] = None
         self._sizes: List[int] = []
+        # overlap ranges: `chunks` when every range keeps >= min_chunk_rows
+        # Gaussians (smaller launches would not fill the GPU)
+        self.chunks = int(chunks if chunks is not None else os.environ.get("GS_ALLREDUCE_CHUNKS", 2))
+        self.min_chunk_rows = int(min_chunk_rows if min_chunk_rows is not None
+                                  else os.environ.get("GS_ALLREDUCE_MIN_ROWS", 1 << 16))
+        self._works: list = []
+        self.ranges_reduced = 0  # rows_ready calls so far (diagnostic)
         # RCCL (backend "nccl") forms the mean inside the reduction (ReduceOp.AVG,
         # NCCL >= 2.10); gloo has no AVG: SUM, then one division.  Decided once.
         self._avg: bool = (dist.is_initialized() and dist.get_backend(group) == "nccl"
@@ -55,6 +71,26 @@ class GradAllReduce:
         model._gs_grad_sink = self
         return self
 
+    def overlap_chunks(self) -> int:
+        """How many Gaussian ranges the render backward should hand to
+        rows_ready (1: one range, reduced as soon as it is done)."""
+        n = self.params[0].shape[0] if self.params else 0
+        return max(1, min(self.chunks, n // max(1, self.min_chunk_rows)))
+
+    def rows_ready(self, lo: int, hi: int) -> None:
+        """Gradient rows [lo, hi) of every parameter are final in the bucket
+        (queued on the current stream): reduce them asynchronously."""
+        flat = self._bucket()
+        n = self.params[0].shape[0]
+        op = self.dist.ReduceOp.AVG if self._avg else self.dist.ReduceOp.SUM
+        self.ranges_reduced += 1
+        off = 0
+        for size in self._sizes:
+            cols = size // n
+            self._works.append(self.dist.all_reduce(flat[off + lo * cols: off + hi * cols], op=op,
+                                                    group=self.group, async_op=True))
+            off += size
+
     def grad_destinations(self, leaves) -> Optional[List[torch.Tensor]]:
         """Bucket views shaped like `leaves`, when every leaf is one of this
         bucket's parameters and none holds a .grad yet (autograd then adopts
@@ -75,6 +111,14 @@ class GradAllReduce:
         flat = self._bucket()
         views = torch.split(flat, self._sizes)
         in_place = [self._aliases(p, v) for p, v in zip(self.params, views)]
+        if self._works:
+            # the backward reduced the bucket range by range (rows_ready)
+            for w in self._works:
+                w.wait()
+            self._works = []
+            if not self._avg:
+                flat.div_(self.dist.get_world_size(self.group))
+            return self._copy_out(views, in_place)
         for p, v, ok in zip(self.params, views, in_place):
             if ok:
                 continue

@@ -301,7 +301,10 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
                       sh_rest=None, sh_degree=0, out=None):
     """out: optional preallocated gradient tensors {name: tensor} (the
     data-parallel bucket's views, distributed.GradAllReduce.attach); the
-    kernels write there instead of into fresh buffers."""
+    kernels write there instead of into fresh buffers.  out["_rows_ready"]
+    (optional): called with (lo, hi) once the gradient rows of Gaussians
+    [lo, hi) are queued, the last stage running in out["_chunks"] ranges so
+    that a range's all-reduce overlaps the next range's kernels."""
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -327,7 +330,9 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         StageTimer.mark("blend_bwd")
         N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
     raw = cov3d is None
-    out = out or {}
+    out = dict(out or {})
+    rows_ready = out.pop("_rows_ready", None)
+    chunks = int(out.pop("_chunks", 1)) if rows_ready is not None else 1
 
     def buf(name, shape):
         t = out.get(name)
@@ -350,9 +355,41 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
                             N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op), N.ptr(d_sh),
                             N.ptr(slot_live), N.ptr(grad_sums))
     StageTimer.mark("project_bwd")
-    N.check(lib.gs_project_backward(C.byref(pb), s), "gs_project_backward")
+    bounds = [n * k // chunks for k in range(chunks + 1)]
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        part = pb if (lo, hi) == (0, n) else _rows_of(pb, lo, hi)
+        N.check(lib.gs_project_backward(C.byref(part), s), "gs_project_backward")
+        if rows_ready is not None:
+            rows_ready(lo, hi)
     StageTimer.mark("~end_bwd")
     return d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh
+
+
+def _rows_of(pb: "N.GsProjectBwdArgs", lo: int, hi: int) -> "N.GsProjectBwdArgs":
+    """The projection backward's arguments restricted to Gaussians [lo, hi):
+    every per-Gaussian pointer advanced by lo rows (the slot partials are
+    addressed through pair_offset, absolute, and stay)."""
+    r = N.GsProjectBwdArgs.from_buffer_copy(pb)
+    g = r.g
+
+    def adv(ptr, row_bytes):
+        return ptr + lo * row_bytes if ptr else ptr
+    g.n = hi - lo
+    g.xyz = adv(g.xyz, 4 * g.xyz_stride)
+    g.cov3d = adv(g.cov3d, 36)
+    g.scaling = adv(g.scaling, 12)
+    g.rotation = adv(g.rotation, 16)
+    g.color_logits = adv(g.color_logits, 4 * g.color_stride)
+    g.opacity = adv(g.opacity, 4 * g.opacity_stride)
+    g.sh_rest = adv(g.sh_rest, 4 * g.sh_rest_stride)
+    for name, rb in (("means2d", 8), ("conics", 16), ("vis", 1), ("rects", 8), ("pair_offset", 4),
+                     ("g_means2d", 8), ("g_conics", 16), ("d_xyz", 12), ("d_cov3d", 36), ("d_scaling", 12),
+                     ("d_rotation", 16), ("d_color_logits", 12), ("d_opacity", 4),
+                     ("d_sh_rest", 4 * N.GS_SH_REST * 3), ("grad_sums", 4 * N.GS_PAIR_GRAD_FLOATS)):
+        setattr(r, name, adv(getattr(r, name), rb))
+    if r.order:
+        raise ValueError("row ranges need the Gaussian-order walk (order = NULL)")
+    return r
 
 
 class RasterizeGaussians(torch.autograd.Function):

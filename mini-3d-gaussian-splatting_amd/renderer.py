@@ -126,7 +126,12 @@ class GaussianRenderer:
 
             def grad_dest():
                 views = sink.grad_destinations(leaves)
-                return None if views is None else dict(zip(names, views))
+                if views is None:
+                    return None
+                d = dict(zip(names, views))
+                if hasattr(sink, "rows_ready"):  # reduce finished ranges during the backward
+                    d["_rows_ready"], d["_chunks"] = sink.rows_ready, sink.overlap_chunks()
+                return d
         image, alpha, depth, means2d, conics, radii, vis = rasterize(
             cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=fused,
             sh_rest=sh_rest, sh_degree=sh_degree, grad_dest=grad_dest)

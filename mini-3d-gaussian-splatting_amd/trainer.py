@@ -103,17 +103,20 @@ class GaussianTrainer:
             g.max_sh_degree = max(g.max_sh_degree, c.sh_degree)
             g.oneup_sh_degree()
         opt.zero_grad()
-        out = self.renderer.render(camera, g, self._settings(camera))
-        target = camera._image
-        total, l1, dssim = photometric_loss(out["image"], target, self.config.lambda_dssim)
-        total.backward()
         if self._dist is not None:
+            # the bucket is attached before the render, so that its backward
+            # writes the gradients into it and reduces them range by range
             params = g.grad_parameters()
             if self._reducer is None or self._reducer_n != g.get_num_points():
                 from .distributed import GradAllReduce
                 self._reducer = GradAllReduce(params, self._dist).attach(g)
                 self._reducer_n = g.get_num_points()
             self._reducer.params = params
+        out = self.renderer.render(camera, g, self._settings(camera))
+        target = camera._image
+        total, l1, dssim = photometric_loss(out["image"], target, self.config.lambda_dssim)
+        total.backward()
+        if self._dist is not None:
             self._reducer.all_reduce_mean()
         opt.update_learning_rate(self.iteration)
         opt.step()

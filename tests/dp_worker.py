@@ -32,7 +32,8 @@ def main():
     tr.train(3)
     torch.cuda.synchronize()
     np.savez(out, **{f"p{i}": p.detach().cpu().numpy() for i, p in enumerate(tr.gaussians.parameter_list())},
-             iteration=tr.iteration, n=tr.gaussians.get_num_points())
+             iteration=tr.iteration, n=tr.gaussians.get_num_points(),
+             ranges=tr._reducer.ranges_reduced if tr._reducer is not None else -1)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -64,7 +64,7 @@ def test_grad_all_reduce_mean_gloo():
         assert torch.equal(res[0][1][i], res[1][1][i])  # replicas stay identical
 
 
-def _worker_zero_copy(rank, world, port, q):
+def _worker_zero_copy(rank, world, port, q, ranges=None):
     import torch.distributed as dist
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -90,6 +90,8 @@ def _worker_zero_copy(rank, world, port, q):
         local = [p.grad.clone() for p in params]
         ptrs = [p.grad.data_ptr() for p in params]
         assert red.grad_destinations(params) is None  # a .grad exists: the kernels need fresh buffers
+        for lo, hi in ranges or ():
+            red.rows_ready(lo, hi)  # what the chunked backward does after each range
         red.all_reduce_mean()
         assert [p.grad.data_ptr() for p in params] == ptrs  # reduced in place, no copies
         q.put((rank, local, [p.grad.clone() for p in params]))
@@ -97,13 +99,16 @@ def _worker_zero_copy(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_grad_all_reduce_zero_copy_gloo():
+@pytest.mark.parametrize("ranges", [None, [(0, 17), (17, 34), (34, 50)]])
+def test_grad_all_reduce_zero_copy_gloo(ranges):
     """The backward writes into the bucket (GradAllReduce.attach): the mean is
-    formed in place and the .grad tensors stay views of the bucket."""
+    formed in place and the .grad tensors stay views of the bucket -- also
+    when the backward hands over row ranges as they finish (rows_ready: one
+    asynchronous all-reduce per parameter slice, waited for in all_reduce_mean)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_zero_copy, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_zero_copy, args=(r, 2, port, q, ranges)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict()

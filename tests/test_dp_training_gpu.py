@@ -54,11 +54,16 @@ def _mean_of_views_reference(pkg, ds, cfg, world):
     return tr
 
 
-def test_dp_trainer_two_ranks_match_mean_of_views(pkg, cuda, tmp_path):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_dp_trainer_two_ranks_match_mean_of_views(pkg, cuda, tmp_path, overlap):
+    """overlap: the render backward hands its gradient rows to the all-reduce
+    in two ranges (GradAllReduce.rows_ready), the first reduced while the
+    second is computed; without: one reduction after the backward."""
     write_scene_files(tmp_path)
     port = _free_port()
     outs = [tmp_path / f"rank{r}.npz" for r in range(2)]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", GS_ALLREDUCE_CHUNKS="2",
+               GS_ALLREDUCE_MIN_ROWS="256" if overlap else str(1 << 30))
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), str(r), "2", str(port),
                                str(tmp_path), str(outs[r])], env=env) for r in range(2)]
     try:
@@ -70,6 +75,8 @@ def test_dp_trainer_two_ranks_match_mean_of_views(pkg, cuda, tmp_path):
     assert rcs == [0, 0], rcs
     a, b = (np.load(o) for o in outs)
     assert int(a["iteration"]) == 3 and int(a["n"]) == int(b["n"])
+    # iteration 3's reducer (rebuilt after the densification): ranges it reduced
+    assert int(a["ranges"]) == (2 if overlap else 1)
     for i in range(6):
         assert np.array_equal(a[f"p{i}"], b[f"p{i}"]), f"replicas diverged in parameter {i}"
     ds = load_scene(pkg, tmp_path, cuda, split=False)

@@ -415,6 +415,30 @@ def test_wide_rects_vs_oracle(pkg, cuda):
     assert not errs, errs
 
 
+class _OneRankDist:
+    """torch.distributed stand-in for one rank: all_reduce is the identity,
+    slices handed to it are recorded."""
+    class ReduceOp:
+        SUM, AVG = "sum", "avg"
+
+    class _Work:
+        def wait(self):
+            return True
+
+    def __init__(self):
+        self.sliced = []
+
+    def is_initialized(self):
+        return False
+
+    def get_world_size(self, group=None):
+        return 1
+
+    def all_reduce(self, t, op=None, group=None, async_op=False):
+        self.sliced.append(t.numel())
+        return self._Work() if async_op else None
+
+
 def test_grad_bucket_adoption(pkg, cuda):
     """GradAllReduce.attach (data-parallel path): the render backward writes
     the gradients straight into the all-reduce bucket and autograd adopts the
@@ -425,12 +449,18 @@ def test_grad_bucket_adoption(pkg, cuda):
     for attach in (False, True):
         m = syn.to_model(sc, pkg.GaussianModel, cuda)
         params = m.grad_parameters()
-        red = pkg.distributed.GradAllReduce(params, dist=object())  # no collective is issued here
+        stub = _OneRankDist()
+        red = pkg.distributed.GradAllReduce(params, dist=stub, min_chunk_rows=4096)
         if attach:
             red.attach(m)
         out = pkg.GaussianRenderer().render(Cam(320, 240, sc.fovx, sc.fovy), m,
                                             pkg.RenderSettings(240, 320, torch.zeros(3)))
         (out["image"].sum() + out["depth"].sum()).backward()
+        if attach:
+            # the backward handed its rows over in two ranges, one slice per parameter each
+            assert red.ranges_reduced == 2 and len(stub.sliced) == 2 * len(params)
+            assert sum(stub.sliced) == sum(p.numel() for p in params)
+            red.all_reduce_mean()
         res.append([p.grad.clone() for p in params])
         if attach:
             for p, v in zip(params, torch.split(red._flat, red._sizes)):
