@@ -962,6 +962,9 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
 #ifndef GS_BWD_GROUP
 #define GS_BWD_GROUP 8
 #endif
+#ifndef GS_BWD_CHUNK_STAGE
+#define GS_BWD_CHUNK_STAGE 1
+#endif
 constexpr int kBwdGroup = GS_BWD_GROUP;  // live entries per phase-B group: 8 or 4
 static_assert(kBwdGroup == 8 || kBwdGroup == 4, "phase B maps 8 or 16 lanes to an entry");
 constexpr int kBwdLanes = kWave / kBwdGroup;  // lanes per entry in phase B (8 or 16)
@@ -1023,7 +1026,13 @@ template <bool kT16>
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
+#if GS_BWD_CHUNK_STAGE
+  // the chunk's records (word 10 = slot), staged per chunk from registers:
+  // 384 B instead of a word's 3 KB, for occupancy (LDS bounds it)
+  __shared__ float2 s_wrec[kBwdGroup * 6];
+#else
   __shared__ float2 s_wrec[kWave * 6];   // the word's live records, packed in bit order; word 10 = slot
+#endif
   const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
   const int ncell = cg.cells();
   int tile, quad;
@@ -1119,7 +1128,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int j = lane / kBwdLanes, sub = lane % kBwdLanes, col = sub & 7, row0 = sub >> 3;
     if (j < k) {
-      const uint32_t e = kb + (uint32_t)j;
+      const uint32_t e = (GS_BWD_CHUNK_STAGE ? 0u : kb) + (uint32_t)j;
       const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * e];  // mx my q00 q11
       const float2 ib = s_wrec[6 * e + 2];                                // qo o
       const uint32_t slot = __float_as_uint(s_wrec[6 * e + 5].x);
@@ -1170,26 +1179,34 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   };
   unsigned long long mcur = live_word(0);  // (word 0's records are in flight already)
   for (uint32_t wd = 0; wd < nwords; ++wd) {
-    // stage the word's live records; word 10 becomes the entry's gradient
-    // slot (the Gaussian's first slot + this tile's index in its rectangle)
+    // word 10 of a live record becomes the entry's gradient slot (the
+    // Gaussian's first slot + this tile's index in its rectangle)
     const bool mine = (mcur >> lane) & 1ull;
+    const uint32_t info = __float_as_uint(r2.w);
+    const uint32_t slot = __float_as_uint(r2.z) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
+                          (tx - (info & 0xFFFu));
+    // packed: the live entry of rank r (bit order) at position r, so a
+    // chunk's records sit at compile-time offsets from one base address
+    const uint32_t rank =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(mcur >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mcur, 0u));
+#if GS_BWD_CHUNK_STAGE
+    // this word's records stay in registers (staged chunk by chunk below)
+    // while the next word's are fetched into r0..r2
+    const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
+#else
     if (mine) {
-      const uint32_t info = __float_as_uint(r2.w);
-      const uint32_t slot = __float_as_uint(r2.z) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
-                            (tx - (info & 0xFFFu));
-      // packed: the live entry of rank r (bit order) at position r, so a
-      // chunk's records sit at compile-time offsets from one base address
-      const uint32_t rank =
-          __builtin_amdgcn_mbcnt_hi((uint32_t)(mcur >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mcur, 0u));
       float4 *d = reinterpret_cast<float4 *>(&s_wrec[6 * rank]);
       d[0] = r0;
       d[1] = r1;
       d[2] = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
     }
+#endif
     const unsigned long long simple_w = __builtin_amdgcn_ballot_w64(mine && simple_entry(r0, r1));
     const unsigned long long mnext = wd + 1u < nwords ? live_word(wd + 1u) : 0ull;
     fetch(wd + 1u, mnext);  // in flight while this word replays
+#if !GS_BWD_CHUNK_STAGE
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
+#endif
     // a word whose live entries are all simple (the common case) runs a copy
     // of the loop without the per-entry test
     auto run_word = [&](auto all_simple_tag) {
@@ -1200,12 +1217,25 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
      // a chunk: the word's next (up to) kBwdGroup live entries
      unsigned long long cm = 0;
      int k = 0;
+#if GS_BWD_CHUNK_STAGE
+     // stage the chunk (ranks kb .. kb + kBwdGroup - 1; the previous chunk's
+     // reads came before these writes in this wave's in-order LDS queue)
+     if (mine && rank - kb < (uint32_t)kBwdGroup) {
+       float4 *d = reinterpret_cast<float4 *>(&s_wrec[6 * (rank - kb)]);
+       d[0] = c0;
+       d[1] = c1;
+       d[2] = c2;
+     }
+     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
+     const char *cb = reinterpret_cast<const char *>(s_wrec);
+#else
      // the chunk's records: one VGPR base (asm: the compiler would otherwise
      // re-materialise it from the SGPR with a v_mov per entry), entry kk at a
      // compile-time offset from it
      uint32_t vb;
      asm volatile("v_mov_b32 %0, %1" : "=v"(vb) : "s"(kb * 48u));
      const char *cb = reinterpret_cast<const char *>(s_wrec) + vb;
+#endif
      // unrolled: the group row k is a compile-time LDS offset
 #pragma unroll
      for (int kk = 0; kk < kBwdGroup; ++kk) {
