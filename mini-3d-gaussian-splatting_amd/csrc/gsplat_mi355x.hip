@@ -1788,9 +1788,12 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
   uint32_t *counts = (uint32_t *)workspace;
   uint32_t *totals = counts + (size_t)kRadix * nb;
   uint32_t *kin = keys, *vin = vals, *kout = keys_alt, *vout = vals_alt;
+  // the bits spread evenly over the passes (13-bit tile ids: 7 + 6, not
+  // 8 + 5): fewer digit runs per block in the first pass, whose scatter
+  // writes are the least coalesced
+  int shift = begin_bit;
   for (int p = 0; p < passes; ++p) {
-    const int shift = begin_bit + p * kRadixBits;
-    const int nbits = (end_bit - shift) < kRadixBits ? (end_bit - shift) : kRadixBits;
+    const int nbits = (end_bit - shift + (passes - p) - 1) / (passes - p);
     k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, nb);
     k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, totals, nb);
     if (p == 0 && vals_are_iota)
@@ -1799,6 +1802,7 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
       k_radix_scatter<false><<<nb, kBlock, 0, s>>>(kin, vin, kout, vout, n, shift, nbits, counts, totals, nb);
     gs_status st = check_launch("gs_radix_sort_pairs");
     if (st) return st;
+    shift += nbits;
     uint32_t *tk = kin, *tv = vin;
     kin = kout;
     vin = vout;

@@ -12,7 +12,10 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(list)
 for f in glob.glob(root + "/p*/pmc_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        k = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"]).split("(")[0]
+        k = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"]).split("(")[0].replace("void ", "")
+        # template arguments dropped (k_blend_fwd<false, true> -> k_blend_fwd), except the
+        # measurement-only counting forward, kept apart
+        k = "k_blend_fwd_counting" if k.startswith("k_blend_fwd<true") else re.sub(r"<.*", "", k)
         if keep and not any(s in k for s in keep):
             continue
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
