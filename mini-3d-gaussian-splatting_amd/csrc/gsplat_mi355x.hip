@@ -24,9 +24,6 @@
 
 namespace {
 
-#ifndef GS_FWD_PREFETCH
-#define GS_FWD_PREFETCH 1
-#endif
 constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kRadixBits = 8;
@@ -876,66 +873,6 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
       // (readfirstlane returns int: widen through uint32_t, never sign-extend)
       unsigned long long m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mw >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mw);
-#if GS_FWD_PREFETCH
-      // Software-pipelined: entry k+1's record (all five pairs, colour and
-      // depth included) is requested before entry k is composited, so its
-      // LDS round trip overlaps entry k's math instead of two round trips
-      // per entry in series.  Unrolled by two with the register sets
-      // swapping roles (no copies); a word's last prefetch re-reads the
-      // current entry (harmless).
-      if (m) {
-        auto rec_at = [&](uint32_t bt) {
-          uint32_t ja;
-          asm volatile("v_mov_b32 %0, %1" : "=v"(ja) : "s"((64u * wd + bt) * 48u));
-          return reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(s_rec) + ja);
-        };
-        auto load = [&](uint32_t bt, float2 (&r)[5]) {
-          const float2 *q = rec_at(bt);
-#pragma unroll
-          for (int i = 0; i < 5; ++i) r[i] = lds_pair(q + i);
-        };
-        // composite entry `bt` from its record r (pm, pq, po, prg, pbz)
-        auto composite = [&](uint32_t bt, const float2 (&r)[5]) {
-          const uint32_t j = 64u * wd + bt;
-          const float dx = fx - r[0].x, dy = fy - r[0].y;
-          const float s = conic_s(dx, dy, r[1].x, r[2].x, r[1].y);  // :333
-          // the :336 skip (w < 1e-5) decided on s, before exp (kSkipS)
-          const bool run = A < kAlphaStop;  // the pixel has not terminated
-          const bool live = run && !(s > kSkipS);
-          if (wave_any(live)) {
-            livem |= 1ull << bt;
-            const float w = sat01(exp_neg_half(s));          // :334
-            const float ai = live ? sat01(r[2].y * w) : 0.f;  // :339 (skips folded, see below)
-            const float c = (1.f - A) * ai;                   // :343-344
-            ar = __builtin_fmaf(c, r[3].x, ar);
-            ag = __builtin_fmaf(c, r[3].y, ag);
-            ab = __builtin_fmaf(c, r[4].x, ab);
-            A = A + c;
-            D = __builtin_fmaf(c, r[4].y, D);
-            if constexpr (kCount) ncontrib += c > 0.f ? 1u : 0u;
-            neval = run ? b - start + j + 1 : neval;
-          }
-        };
-        float2 ra[5], rb[5];
-        uint32_t bit_a = (uint32_t)__builtin_ctzll(m), bit_b;
-        m &= m - 1ull;
-        load(bit_a, ra);
-        while (true) {
-          bool more = m != 0ull;
-          bit_b = more ? (uint32_t)__builtin_ctzll(m) : bit_a;
-          m &= m - 1ull;
-          load(bit_b, rb);
-          composite(bit_a, ra);
-          if (!more) break;
-          more = m != 0ull;
-          bit_a = more ? (uint32_t)__builtin_ctzll(m) : bit_b;
-          m &= m - 1ull;
-          load(bit_a, ra);
-          composite(bit_b, rb);
-          if (!more) break;
-        }
-      }
-#else
       while (m) {
         const uint32_t bit = (uint32_t)__builtin_ctzll(m);
         m &= ~(1ull << bit);
@@ -977,7 +914,6 @@ __global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
           neval = run ? b - start + j + 1 : neval;
         }
       }
-#endif
       // (only words inside the tile's list: the next tile's words follow)
       if (lane == 0 && b - start + 64u * wd < end - start && live_word0 + wd < (uint64_t)a.live_words)
         a.live_bits[(size_t)qi * a.live_words + live_word0 + wd] = livem;
