@@ -186,8 +186,8 @@ gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream);
  * renderer.py:273-367: per pixel (integer coordinates) front-to-back alpha
  * compositing of its tile's list, termination once A >= 0.995, background
  * composite (bg counted twice, as the reference does), clamps, depth
- * normalisation.  One 256-thread workgroup per 2x2 cells of a tile (the
- * whole tile at the default tile_size 16), sharing the tile's list.  pix_state
+ * normalisation.  One 64-lane workgroup per (tile, 8x8 cell), the cells of
+ * a tile independent of each other, each walking the tile's list.  pix_state
  * keeps what the backward needs: [H*W] float4 (acc_r, acc_g, acc_b, D) and
  * [H*W] float2 (A, bits of n_eval). */
 typedef struct gs_blend_fwd_args {

@@ -740,42 +740,14 @@ __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
 // ======================================================== blend fwd =======
 // Cells: a tile of edge L (GaussianRenderer.tile_size) is covered from its
 // origin by QX x QX cells of 8x8 pixels, QX = ceil(L/8) (edge cells clipped
-// to the tile); a wave renders one cell, lane l its pixel (l&7, l>>3) --
-// compact footprints per wave keep the per-pair branches coherent.  A
-// 256-thread forward block renders a 2x2 group of cells of one tile (the
-// whole tile when L = 16), all blending that tile's list: group g of the
-// tile's GX x GX groups (GX = ceil(QX/2)), wave w its cell (w&1, w>>1).
+// to the tile); a wave renders one cell, lane l its pixel (l&7, l>>3), and
+// blends the tile's whole list (renderer.py:302-319).  L = 16: the tile's
+// four 8x8 quadrants.
 struct CellGeom {
-  int L, QX, GX;
-  __device__ explicit CellGeom(int tile_size) : L(tile_size), QX((tile_size + 7) >> 3), GX((QX + 1) >> 1) {}
+  int L, QX;
+  __device__ explicit CellGeom(int tile_size) : L(tile_size), QX((tile_size + 7) >> 3) {}
   __device__ int cells() const { return QX * QX; }
-  __device__ int groups() const { return GX * GX; }
 };
-
-// Wave-level culling of list entries.  Bit q of the result is clear only if
-// every pixel centre of the tile's 8x8 quadrant q = (q&1, q>>1) provably has
-// s > 23.1, i.e. exp(-s/2) < 1e-5 (the :336 skip): that wave may pass the
-// entry over without evaluating it (each lane's own exact test still decides
-// the rest).  The s <= L ellipse, L = 23.1 * 1.01, lies in the box
-// |x - mx| <= sqrt(L Sxx), |y - my| <= sqrt(L Syy), Sigma = Q^-1 for the form
-// Q = [[q00, qo/2], [qo/2, q11]] the blend evaluates.  The 1% margin covers
-// the fp32 rounding of s: |s_fp32 - s| <= ~4u (q00 dx^2 + |qo dx dy| + q11 dy^2)
-// <= 4u (tr + |qo|) tr / det * s, so conics with (tr + |qo|) tr > 1e4 det --
-// and non-positive-definite or NaN ones -- keep all four bits.
-__device__ __forceinline__ uint32_t quad_mask(float mx, float my, float q00, float qo, float q11, float x0,
-                                              float y0) {
-  const float q01 = 0.5f * qo;
-  const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
-  if (!(tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det)) return 0xFu;
-  const float L = 23.1f * 1.01f;
-  // v_rcp / v_sqrt (~1 ulp): far inside the 1% margin
-  const float id = __builtin_amdgcn_rcpf(det);
-  const float hx = __builtin_amdgcn_sqrtf(L * q11 * id), hy = __builtin_amdgcn_sqrtf(L * q00 * id);
-  const bool x0h = mx + hx >= x0 && mx - hx <= x0 + 7.f, x1h = mx + hx >= x0 + 8.f && mx - hx <= x0 + 15.f;
-  const bool y0h = my + hy >= y0 && my - hy <= y0 + 7.f, y1h = my + hy >= y0 + 8.f && my - hy <= y0 + 15.f;
-  return (uint32_t)(x0h && y0h) | ((uint32_t)(x1h && y0h) << 1) | ((uint32_t)(x0h && y1h) << 2) |
-         ((uint32_t)(x1h && y1h) << 3);
-}
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
@@ -793,139 +765,139 @@ __device__ __forceinline__ float2 lds_pair(const float2 *p) {
   return make_float2(__uint_as_float((uint32_t)v), __uint_as_float((uint32_t)(v >> 32)));
 }
 
+// Wave-level culling of list entries: false only if every pixel centre of
+// the 8x8 box [x0, x0 + 7] x [y0, y0 + 7] provably has s > 23.1, i.e.
+// exp(-s/2) < 1e-5 (the :336 skip): the cell's wave may pass the entry over
+// without evaluating it (each lane's own exact test still decides the rest).
+// The s <= L ellipse, L = 23.1 * 1.01, lies in the box |x - mx| <= sqrt(L Sxx),
+// |y - my| <= sqrt(L Syy), Sigma = Q^-1 for the form Q = [[q00, qo/2],
+// [qo/2, q11]] the blend evaluates.  The 1% margin covers the fp32 rounding of
+// s: |s_fp32 - s| <= ~4u (q00 dx^2 + |qo dx dy| + q11 dy^2) <= 4u (tr + |qo|)
+// tr / det * s, so conics with (tr + |qo|) tr > 1e4 det -- and
+// non-positive-definite or NaN ones -- are never culled.
+__device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo, float q11, float x0, float y0) {
+  const float q01 = 0.5f * qo;
+  const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
+  if (!(tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det)) return true;
+  const float L = 23.1f * 1.01f;
+  // v_rcp / v_sqrt (~1 ulp): far inside the 1% margin
+  const float id = __builtin_amdgcn_rcpf(det);
+  const float hx = __builtin_amdgcn_sqrtf(L * q11 * id), hy = __builtin_amdgcn_sqrtf(L * q00 * id);
+  return mx + hx >= x0 && mx - hx <= x0 + 7.f && my + hy >= y0 && my - hy <= y0 + 7.f;
+}
+
+// Workgroup b -> (tile, cell): b, b+8, b+16, ... share an XCD (round-robin
+// dispatch; placement is for speed only), so the Q cells of a tile read its
+// records through one L2.  Grid: ceil(tiles / 8) * 8 Q.
+__device__ __forceinline__ void cell_tile(uint32_t b, int ncell, int &tile, int &quad) {
+  const uint32_t grp = b >> 3;
+  const uint32_t q = (uint32_t)ncell;
+  quad = (int)(grp % q);
+  tile = (int)((grp / q) * 8u + (b & 7u));
+}
+
+// Forward blend, one 64-lane workgroup per (tile, 8x8 cell), lane = pixel
+// (compact footprints keep the per-pair branches coherent).  The cells of a
+// tile run independently (no barrier): each stages its own batches of 64
+// records in LDS (the next batch gathered into registers meanwhile), culls
+// them against its own box (cell_hit, one ballot per batch) and walks the set
+// bits.  Round 1 shared the staging between the four cells of a 16x16 tile
+// in a 256-thread block and paid, at every barrier, for its busiest wave;
+// here a cell's time is its own work, the records re-read per cell from the
+// L2 the tile's cells share (8 us less at C3).  Control flow stays
+// wave-uniform (ballots, scalar bit scans); per-lane decisions are
+// predicates, and a skipped pair adds exact zeros: the :336 / :340 / :345
+// skips are folded into the weight (a skipped pair gets ai = 0, hence
+// c = (1 - A) * 0 = +0, and an accepted one c = (1 - A) * ai > 0 -- the
+// reference's c exactly), v_cndmask selects instead of SGPR mask arithmetic.
+// Each cell writes a liveness word per 64 entries for the backward
+// (gs_blend_live_words).
 // kCount: also count each pixel's contributing pairs (c > 0) into
 // a.pair_counts -- a work counter for the measurement, off in the
-// render path.
-// kT16: tile_size is the default 16 (its cell geometry folds to constants).
+// render path.  kT16: tile_size is the default 16 (its cell geometry folds to
+// constants).
 template <bool kCount, bool kT16>
-__global__ __launch_bounds__(kBlock) void k_blend_fwd(gs_blend_fwd_args a) {
-  __shared__ float2 s_rec[kBlock * 6];
+__global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
+  __shared__ float2 s_rec[kWave * 6];
   const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
-  const int ng = cg.groups();
-  const int tile = (int)blockIdx.x / ng, grp = (int)blockIdx.x - tile * ng;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int gx = grp % cg.GX, gy = grp / cg.GX;
-  const int qx = 2 * gx + (wave & 1), qy = 2 * gy + (wave >> 1);
-  const int lx = qx * 8 + (lane & 7), ly = qy * 8 + (lane >> 3);  // tile-relative pixel
-  const int tox = (tile % a.tiles_x) * cg.L, toy = (tile / a.tiles_x) * cg.L;
-  const int px = tox + lx, py = toy + ly;
+  const int ncell = cg.cells();
+  int tile, quad;
+  cell_tile(blockIdx.x, ncell, tile, quad);
+  if (tile >= a.tiles_x * a.tiles_y) return;
+  const int lane = threadIdx.x;
+  const int cx0 = (quad % cg.QX) * 8, cy0 = (quad / cg.QX) * 8;  // the cell in its tile
+  const int x0 = (tile % a.tiles_x) * cg.L + cx0, y0 = (tile / a.tiles_x) * cg.L + cy0;
+  const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
   const int W = a.cam.image_width, H = a.cam.image_height;
-  const bool inside = lx < cg.L && ly < cg.L && px < W && py < H;
-  // (a cell past the tile's QX x QX has no pixel inside: its wave is done at once)
-  const int qi = qy * cg.QX + qx;
+  const bool inside = cx0 + (lane & 7) < cg.L && cy0 + (lane >> 3) < cg.L && px < W && py < H;
   const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]),
                  end = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
   float ar = bg0, ag = bg1, ab = bg2;  // out_rgb = bg (renderer.py:273)
-  // A lane is done once A >= kAlphaStop (A only grows through accepted
-  // pairs, so that is exactly the :352 break); lanes outside the tile or
-  // image start done.  No loop-carried bool: "done" is one compare, not a
-  // mask in SGPRs.
+  // a lane is done once A >= kAlphaStop (the :352 break); lanes outside the
+  // tile or image start done
   float A = inside ? 0.f : 1.f, D = 0.f;
   uint32_t neval = 0, ncontrib = 0;
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
-  __shared__ uint32_t s_live[4];
-  // s_qm[q][w]: bit i set if entry 64w+i of the batch may reach cell q of the group
-  __shared__ unsigned long long s_qm[4][4];
-  // the group's 16x16 box, for the per-cell culling masks
-  const float tx0 = (float)(tox + 16 * gx), ty0 = (float)(toy + 16 * gy);
-  // batch i+1's records are gathered into registers while batch i composites
+  // liveness word of (this batch, this cell): see gs_blend_live_words
+  uint64_t *live = a.live_bits + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile;
+  const uint64_t live_left = (uint64_t)a.live_words - (start / 64u + (uint32_t)tile);
   float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
-  if (start + threadIdx.x < end) {
-    const uint32_t gid = a.sorted_gauss[start + threadIdx.x];
+  if (start + (uint32_t)lane < end) {
+    const uint32_t gid = a.sorted_gauss[start + lane];
     n0 = recs[3 * (size_t)gid];
     n1 = recs[3 * (size_t)gid + 1];
     n2 = recs[3 * (size_t)gid + 2];
   }
-  for (uint32_t b = start; b < end; b += kBlock) {
-    {  // (the previous round ended in a barrier after its last LDS read)
-      float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * threadIdx.x]);
-      d[0] = n0;
-      d[1] = n1;
-      d[2] = n2;
-      const uint32_t qm = (b + threadIdx.x < end) ? quad_mask(n0.x, n0.y, n0.z, n1.x, n0.w, tx0, ty0) : 0u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const unsigned long long bq = __builtin_amdgcn_ballot_w64((qm >> q) & 1u);
-        if (lane == 0) s_qm[q][wave] = bq;
-      }
-    }
-    lds_barrier();
-    if (b + kBlock + threadIdx.x < end) {
-      const uint32_t gid = a.sorted_gauss[b + kBlock + threadIdx.x];
+  for (uint32_t b = start; b < end; b += kWave) {
+    if (!wave_any(A < kAlphaStop)) break;  // every pixel of the cell done
+    // stage the batch (this wave's own earlier reads precede these writes)
+    float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * lane]);
+    d[0] = n0;
+    d[1] = n1;
+    d[2] = n2;
+    const bool hit = b + (uint32_t)lane < end && cell_hit(n0.x, n0.y, n0.z, n1.x, n0.w, (float)x0, (float)y0);
+    const unsigned long long mw = __builtin_amdgcn_ballot_w64(hit);
+    unsigned long long m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mw >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mw);
+    // the next batch's records in flight while this one composites
+    if (b + kWave + (uint32_t)lane < end) {
+      const uint32_t gid = a.sorted_gauss[b + kWave + lane];
       n0 = recs[3 * (size_t)gid];
       n1 = recs[3 * (size_t)gid + 1];
       n2 = recs[3 * (size_t)gid + 2];
     }
-    // Control flow stays wave-uniform (ballots, scalar bit scans over the
-    // quadrant masks); per-lane decisions are predicates, and a skipped pair
-    // adds exact zeros.
-    // The "every lane done" exit is tested once per 64-entry word: past it
-    // an entry costs only the s test (A >= kAlphaStop fails every lane), far
-    // less than a per-entry ballot + branch on the whole list.
-    // liveness word of (this batch, word wd, this quadrant): see gs_blend_live_words
-    const uint64_t live_word0 = (uint64_t)start / 64u + (uint64_t)tile + (uint64_t)(b - start) / 64u;
-    for (int wd = 0; wd < 4; ++wd) {
-      if (!wave_any(A < kAlphaStop)) break;
-      unsigned long long livem = 0;  // entries some lane of this wave evaluated
-      const unsigned long long mw = s_qm[wave][wd];
-      // (readfirstlane returns int: widen through uint32_t, never sign-extend)
-      unsigned long long m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mw >> 32)) << 32) |
-                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mw);
-      while (m) {
-        const uint32_t bit = (uint32_t)__builtin_ctzll(m);
-        m &= ~(1ull << bit);
-        const uint32_t j = 64u * wd + bit;
-        // pq = (q00, q11), po = (qo, opacity)
-        // the entry's LDS address in a pinned VGPR (asm: not re-materialised
-        // from the SGPR for the colour/depth reads below, a VALU saved)
-        uint32_t ja;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(ja) : "s"(j * 48u));
-        const float2 *rj = reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(s_rec) + ja);
-        const float2 pm = lds_pair(rj), pq = lds_pair(rj + 1), po = lds_pair(rj + 2);
-        const float dx = fx - pm.x, dy = fy - pm.y;
-        const float s = conic_s(dx, dy, pq.x, po.x, pq.y);  // :333
-        // the :336 skip (w < 1e-5) decided on s, before exp (kSkipS)
-        const bool run = A < kAlphaStop;  // the pixel has not terminated
-        const bool live = run && !(s > kSkipS);
-        if (wave_any(live)) {
-          livem |= 1ull << bit;
-          const float w = sat01(exp_neg_half(s));  // :334
-          // :336 / :340 / :345 skips folded into the weight: a skipped pair
-          // gets ai = 0, hence c = (1 - A) * 0 = +0 (1 - A >= 0), and an
-          // accepted one c = (1 - A) * ai > 0 -- the reference's c exactly.
-          // Selects (v_cndmask) instead of SGPR mask arithmetic.
-          const float ai = live ? sat01(po.y * w) : 0.f;  // :339
-          const float c = (1.f - A) * ai;                                        // :343-344
-          const float2 prg = lds_pair(rj + 3), pbz = lds_pair(rj + 4);
-          // colour / depth sums fused (one rounding per term): they decide
-          // nothing -- termination reads A only -- and the backward reads
-          // their totals
-          ar = __builtin_fmaf(c, prg.x, ar);
-          ag = __builtin_fmaf(c, prg.y, ag);
-          ab = __builtin_fmaf(c, pbz.x, ab);
-          A = A + c;
-          D = __builtin_fmaf(c, pbz.y, D);
-          if constexpr (kCount) ncontrib += c > 0.f ? 1u : 0u;
-          // :352 (after accumulation): the terminating entry is the last one
-          // reached while the pixel still ran (A only grows; a pixel still
-          // running at the end of its list gets end - start below)
-          neval = run ? b - start + j + 1 : neval;
-        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
+    unsigned long long livem = 0;  // entries some lane of this cell evaluated
+    while (m) {
+      const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+      m &= ~(1ull << bit);
+      uint32_t ja;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(ja) : "s"(bit * 48u));
+      const float2 *rj = reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(s_rec) + ja);
+      const float2 pm = lds_pair(rj), pq = lds_pair(rj + 1), po = lds_pair(rj + 2);
+      const float dx = fx - pm.x, dy = fy - pm.y;
+      const float s = conic_s(dx, dy, pq.x, po.x, pq.y);  // :333
+      const bool run = A < kAlphaStop;
+      const bool lv = run && !(s > kSkipS);  // the :336 skip, decided on s
+      if (wave_any(lv)) {
+        livem |= 1ull << bit;
+        const float w = sat01(exp_neg_half(s));          // :334
+        const float ai = lv ? sat01(po.y * w) : 0.f;      // :339 (skips folded into the weight)
+        const float c = (1.f - A) * ai;                   // :343-344
+        const float2 prg = lds_pair(rj + 3), pbz = lds_pair(rj + 4);
+        ar = __builtin_fmaf(c, prg.x, ar);
+        ag = __builtin_fmaf(c, prg.y, ag);
+        ab = __builtin_fmaf(c, pbz.x, ab);
+        A = A + c;
+        D = __builtin_fmaf(c, pbz.y, D);
+        if constexpr (kCount) ncontrib += c > 0.f ? 1u : 0u;
+        neval = run ? b - start + bit + 1 : neval;  // :352, see k_blend_fwd
       }
-      // (only words inside the tile's list: the next tile's words follow)
-      if (lane == 0 && b - start + 64u * wd < end - start && live_word0 + wd < (uint64_t)a.live_words)
-        a.live_bits[(size_t)qi * a.live_words + live_word0 + wd] = livem;
     }
-    // all pixels of the tile done? (per-wave ballot -- taken with every lane
-    // active, outside the lane-0 branch -- then the 4 wave flags)
-    const bool wave_live = wave_any(A < kAlphaStop);
-    if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = wave_live ? 1u : 0u;
-    lds_barrier();
-    const uint32_t any_live = s_live[0] | s_live[1] | s_live[2] | s_live[3];
-    lds_barrier();  // s_live / s_rec reads done before the next round writes them
-    if (!any_live) break;
+    const uint64_t wi = (b - start) / 64u;
+    if (lane == 0 && wi < live_left) live[wi] = livem;
   }
   if (!inside) return;
   if (A < kAlphaStop) neval = end - start;
@@ -1002,7 +974,7 @@ __device__ __forceinline__ float oct_sum(float v) {
 }
 
 // An entry whose clamps provably never bind: opacity in [1e-20, 1] and a
-// conic passing quad_mask's conditioning test (positive definite, fp32 s >= 0
+// conic passing cell_hit's conditioning test (positive definite, fp32 s >= 0
 // at every pixel).  Then exp(-s/2) <= 1 and o w <= 1, and an accepted pair
 // has c = (1 - A) o w >= 0.005 * 1e-20 * 1e-5 > 0.
 __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
@@ -1012,15 +984,6 @@ __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
   return o >= 1e-20f && o <= 1.f && tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det;
 }
 
-// Workgroup b -> (tile, cell): b, b+8, b+16, ... share an XCD (round-robin
-// dispatch; placement is for speed only), so the Q cells of a tile read its
-// records through one L2.  Grid: ceil(tiles / 8) * 8 Q.
-__device__ __forceinline__ void quad_tile(int ncell, int &tile, int &quad) {
-  const uint32_t b = blockIdx.x, grp = b >> 3;
-  const uint32_t q = (uint32_t)ncell;
-  quad = (int)(grp % q);
-  tile = (int)((grp / q) * 8u + (b & 7u));
-}
 
 template <bool kT16>
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
@@ -1036,7 +999,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
   const int ncell = cg.cells();
   int tile, quad;
-  quad_tile(ncell, tile, quad);
+  cell_tile(blockIdx.x, ncell, tile, quad);
   if (tile >= a.tiles_x * a.tiles_y) return;
   const int lane = threadIdx.x;
   const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
@@ -1871,17 +1834,15 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
       !a->live_bits || a->live_words <= 0)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_forward");
   hipStream_t s = (hipStream_t)stream;
-  const int gx = ((a->cam.tile_size + GS_QUAD - 1) / GS_QUAD + 1) / 2;  // 2x2 cell groups per tile axis
-  const long long blocks = (long long)a->tiles_x * a->tiles_y * gx * gx;
-  if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_forward");
-  if (blocks == 0) return GS_OK;
   const bool t16 = a->cam.tile_size == GS_DEFAULT_TILE;
+  const long long cblocks = (long long)div_up((long long)a->tiles_x * a->tiles_y, 8) * 8LL * cells_per_tile(a->cam.tile_size);
+  if (cblocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_forward");
   if (a->pair_counts)
-    k_blend_fwd<true, false><<<(unsigned)blocks, kBlock, 0, s>>>(*a);
+    k_blend_fwd<true, false><<<(unsigned)cblocks, kWave, 0, s>>>(*a);
   else if (t16)
-    k_blend_fwd<false, true><<<(unsigned)blocks, kBlock, 0, s>>>(*a);
+    k_blend_fwd<false, true><<<(unsigned)cblocks, kWave, 0, s>>>(*a);
   else
-    k_blend_fwd<false, false><<<(unsigned)blocks, kBlock, 0, s>>>(*a);
+    k_blend_fwd<false, false><<<(unsigned)cblocks, kWave, 0, s>>>(*a);
   return check_launch("gs_blend_forward");
 }
 
