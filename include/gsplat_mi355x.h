@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 7
+#define GS_ABI_VERSION 8
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
@@ -45,7 +45,8 @@ extern "C" {
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian, 8x8 cell) gradient partial */
 #define GS_PARTIAL_STRIDE 12   /* floats between partials in pair_grads (10 used; 16-B aligned) */
-#define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2..3] reserved */
+#define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2] / [3] min / max fp32 bits of the
+                                 visible depths (0xFFFFFFFF / 0 when none; see gs_project_args) */
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -120,7 +121,20 @@ typedef struct gs_project_args {
   uint8_t *vis;         /* [n]   torch.bool storage */
   float *records;       /* [n, GS_RECORD_FLOATS] */
   uint32_t *rects;      /* [n,2] packed tile rectangle */
-  uint32_t *depth_keys; /* [n]   fp32 bits of Z if visible, else 0xFFFFFFFF */
+  uint32_t *depth_keys; /* [n]   depth sort keys, see key_base */
+  /* Depth keys for the sort of renderer.py:231-237.  Z > 0 for a visible
+   * Gaussian, so the fp32 bits of Z order as the depths do: a visible g gets
+   * depth_keys[g] = bits(Z) - key_base, a culled one 2^key_bits - 1 (last).
+   * key_base = 0, key_bits = 32 is the plain float order.  A caller that
+   * knows the visible depth range (counters[2..3] of the previous frame,
+   * gs_bin_count) may window it to fewer bits and sort bits [0, key_bits):
+   * one radix pass less per 8 bits.  The keys are exact only if every
+   * visible bits(Z) - key_base < 2^key_bits - 1, which this frame's
+   * counters[2..3] tell after gs_bin_count: otherwise sort again with 32. */
+  uint32_t key_base;
+  int32_t key_bits;     /* 1..32 */
+  uint32_t *key_minmax; /* [2 * ceil(n / 256)] per-block min / max of the visible bits(Z), for
+                           gs_bin_count's counters[2..3] */
 } gs_project_args;
 gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream);
 
@@ -158,6 +172,7 @@ typedef struct gs_bin_args {
   const uint32_t *rects;      /* [n,2] from gs_project_forward */
   const uint8_t *vis;         /* [n]   from gs_project_forward */
   uint32_t *counters;         /* [GS_NUM_COUNTERS] */
+  const uint32_t *key_minmax; /* gs_project_args.key_minmax (reduced into counters[2..3]) */
   void *workspace;
   size_t workspace_bytes;
   /* emit outputs (tile_keys / pair_gauss / records ignored by gs_bin_count) */

@@ -27,7 +27,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 12  # floats between quadrant partials in pair_grads
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 7
+GS_ABI_VERSION = 8
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -55,13 +55,15 @@ class GsProjectArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("g", GsGaussians), ("means2d", _vp), ("conics", _vp), ("radii", _vp),
         ("vis", _vp), ("records", _vp), ("rects", _vp), ("depth_keys", _vp),
+        ("key_base", C.c_uint32), ("key_bits", C.c_int32), ("key_minmax", _vp),
     ]
 
 
 class GsBinArgs(C.Structure):
     _fields_ = [
         ("n", C.c_int32), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("sorted_ids", _vp),
-        ("rects", _vp), ("vis", _vp), ("counters", _vp), ("workspace", _vp), ("workspace_bytes", C.c_size_t),
+        ("rects", _vp), ("vis", _vp), ("counters", _vp), ("key_minmax", _vp), ("workspace", _vp),
+        ("workspace_bytes", C.c_size_t),
         ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp), ("records", _vp),
         ("capacity", C.c_int64),
     ]

@@ -278,8 +278,10 @@ __device__ __forceinline__ void color_logits(const gs_gaussians &G, const gs_cam
 // further round trips).
 template <bool kHot>
 __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
+  __shared__ uint32_t s_mm[2][kBlock / kWave];
   const int g = blockIdx.x * kBlock + threadIdx.x;
   bool visible = false;
+  uint32_t zbits = 0u;
   if (g < a.g.n) {
     const gs_camera &c = a.cam;
     const float *X3 = a.g.xyz + (int64_t)g * a.g.xyz_stride;
@@ -391,7 +393,32 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
       rec[2] = make_float4(cb, Z, 0.f, __uint_as_float(rinfo));
     }
     reinterpret_cast<uint2 *>(a.rects)[g] = make_uint2(rx, ry);
-    a.depth_keys[g] = visible ? __float_as_uint(Z) : 0xFFFFFFFFu;
+    zbits = __float_as_uint(Z);
+    const uint32_t kmask = a.key_bits >= 32 ? 0xFFFFFFFFu : (1u << a.key_bits) - 1u;
+    // (a key outside the window is caught by the caller from counters[2..3])
+    a.depth_keys[g] = visible ? ((zbits - a.key_base) & kmask) : kmask;
+  }
+  // the block's min / max of the visible depth bits (plain stores, reduced by gs_bin_count)
+  uint32_t mn = visible ? zbits : 0xFFFFFFFFu, mx = visible ? zbits : 0u;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, d, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+  }
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_mm[0][wave] = mn;
+    s_mm[1][wave] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 1; w < kBlock / kWave; ++w) {
+      mn = min(mn, s_mm[0][w]);
+      mx = max(mx, s_mm[1][w]);
+    }
+    a.key_minmax[2 * blockIdx.x] = mn;
+    a.key_minmax[2 * blockIdx.x + 1] = mx;
   }
 }
 
@@ -537,7 +564,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
 }
 
 // ======================================================== binning =========
-// partials[0..nb): touches per block, partials[nb..2nb): visible per block
+// partials[0..nb): touches per block, partials[nb..2nb): visible per block,
+// [2nb..3nb): index-order slots per chunk, [3nb..5nb): depth-bits min / max per chunk
 __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials, int nb) {
   __shared__ uint32_t s_tmp[4];
   const long long base = (long long)blockIdx.x * kBinChunk;
@@ -596,11 +624,31 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
     carry += t;
   }
   if (threadIdx.x == 0) partials[2 * nb + blockIdx.x] = carry;
+  // the projection blocks of this chunk (kBinChunk / kBlock of them): their
+  // depth-bits min / max, folded for k_bin_scan_partials
+  constexpr int kPB = kBinChunk / kBlock;
+  if (threadIdx.x < kPB) {
+    const int pb = blockIdx.x * kPB + threadIdx.x, npb = (a.n + kBlock - 1) / kBlock;
+    const bool ok = pb < npb;
+    uint32_t mn = ok ? a.key_minmax[2 * pb] : 0xFFFFFFFFu, mx = ok ? a.key_minmax[2 * pb + 1] : 0u;
+#pragma unroll
+    for (int d = 1; d < kPB; d <<= 1) {
+      mn = min(mn, (uint32_t)__shfl_xor((int)mn, d, 64));
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+    }
+    if (threadIdx.x == 0) {
+      partials[3 * nb + blockIdx.x] = mn;
+      partials[4 * nb + blockIdx.x] = mx;
+    }
+  }
 }
 
-// exclusive scan of the touch partials (single block); counters[0] = M, [1] = T
+// exclusive scan of the touch partials (single block); counters[0] = M, [1] = T,
+// [2] / [3] = min / max visible depth bits (the projection's per-block values)
 __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials, int nb, uint32_t *counters) {
   __shared__ uint32_t s_tmp[4];
+  __shared__ uint32_t s_mm[2][kBlock / kWave];
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
   uint32_t carry = 0, vis = 0, slots = 0, tot;
   // a chunk's three partials loaded unconditionally (clamped index) and the
   // next chunk's in flight during this one's scans: no load waits under a
@@ -610,12 +658,17 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
     v[0] = partials[ci];
     v[1] = partials[nb + ci];
     v[2] = partials[2 * nb + ci];
+    v[3] = partials[3 * nb + ci];
+    v[4] = partials[4 * nb + ci];
   };
-  uint32_t vn[3];
+  uint32_t vn[5];
   ld((int)threadIdx.x, vn);
   for (int c = 0; c < nb; c += kBlock) {
     const int i = c + threadIdx.x;
     const uint32_t v0 = i < nb ? vn[0] : 0u, v1 = i < nb ? vn[1] : 0u, v2 = i < nb ? vn[2] : 0u;
+    // (a clamped reload of the last chunk only repeats a value: harmless for min / max)
+    mn = min(mn, vn[3]);
+    mx = max(mx, vn[4]);
     ld(i + kBlock, vn);
     const uint32_t e0 = block_exscan(v0, s_tmp, &tot);
     if (i < nb) partials[i] = carry + e0;
@@ -627,11 +680,26 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
     if (i < nb) partials[2 * nb + i] = slots + e2;
     slots += tot;
   }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, d, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    s_mm[0][threadIdx.x >> 6] = mn;
+    s_mm[1][threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();  // s_mm
   if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 0; w < kBlock / kWave; ++w) {
+      mn = min(mn, s_mm[0][w]);
+      mx = max(mx, s_mm[1][w]);
+    }
     counters[0] = vis;
     counters[1] = carry;
-    counters[2] = 0;
-    counters[3] = 0;
+    counters[2] = mn;
+    counters[3] = mx;
   }
 }
 
@@ -1711,11 +1779,12 @@ gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream) {
   if (!rect_ok(a->cam))
     return fail(GS_ERR_UNSUPPORTED, "%s: radius_min <= radius_max, finite, with rectangles of at most 256 tiles in x "
                 "(GS_MAX_RECT_TILES)", "gs_project_forward");
+  if (a->key_bits < 1 || a->key_bits > 32) return fail(GS_ERR_INVALID_ARG, "%s: key_bits must be 1..32", "gs_project_forward");
   if (a->g.n < 0) return fail(GS_ERR_INVALID_ARG, "%s: bad n", "gs_project_forward");
   hipStream_t s = (hipStream_t)stream;
   if (a->g.n == 0) return GS_OK;
   if (!a->g.xyz || !a->g.color_logits || !a->g.opacity || !a->means2d || !a->conics || !a->radii ||
-      !a->vis || !a->records || !a->rects || !a->depth_keys)
+      !a->vis || !a->records || !a->rects || !a->depth_keys || !a->key_minmax)
     return fail(GS_ERR_INVALID_ARG, "%s: null pointer", "gs_project_forward");
   if (!a->g.cov3d && (!a->g.scaling || !a->g.rotation))
     return fail(GS_ERR_INVALID_ARG, "%s: need cov3d or scaling+rotation", "gs_project_forward");
@@ -1776,13 +1845,13 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
 }
 
 size_t gs_bin_workspace_bytes(int32_t n) {
-  return 3 * sizeof(uint32_t) * (size_t)(n > 0 ? div_up(n, kBinChunk) : 1) + 256;
+  return 5 * sizeof(uint32_t) * (size_t)(n > 0 ? div_up(n, kBinChunk) : 1) + 256;
 }
 
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
   if (!a || !a->counters) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_bin_count");
   if (a->n <= 0) return GS_OK;
-  if (!a->sorted_ids || !a->rects || !a->vis || !a->pair_offset || !a->workspace ||
+  if (!a->sorted_ids || !a->rects || !a->vis || !a->pair_offset || !a->workspace || !a->key_minmax ||
       a->workspace_bytes < gs_bin_workspace_bytes(a->n))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer or workspace too small", "gs_bin_count");
   hipStream_t s = (hipStream_t)stream;

@@ -149,7 +149,29 @@ class _Frame:
 
 
 _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess)
-_HOST_COUNTERS: dict = {}  # device -> pinned int32[2] for the (M, T) read-back
+_HOST_COUNTERS: dict = {}  # device -> pinned int32[4] for the (M, T, depth-bits range) read-back
+_DEPTH_WINDOW: dict = {}  # device -> (key_base, key_bits) from its last frame's visible depth range
+
+
+def depth_window(zmin_bits: int, zmax_bits: int):
+    """(key_base, key_bits) of a window around the visible fp32 depth bits
+    [zmin_bits, zmax_bits], widened by 1/8 of the range on both sides for the
+    next frame's drift; None when no pass would be saved (32 bits anyway)."""
+    if zmin_bits > zmax_bits:
+        return None
+    span = zmax_bits - zmin_bits
+    lo = max(0, zmin_bits - span // 8 - 1)
+    hi = zmax_bits + span // 8 + 1
+    bits = max(1, (hi - lo + 1).bit_length())  # keys 0 .. hi - lo < 2^bits - 1 (the culled sentinel)
+    return (lo, bits) if (bits + 7) // 8 < 4 else None
+
+
+def window_holds(window, zmin_bits: int, zmax_bits: int) -> bool:
+    """Did every visible key of this frame fit the window it was sorted with?"""
+    if window is None or zmin_bits > zmax_bits:
+        return True
+    base, bits = window
+    return zmin_bits >= base and zmax_bits - base < (1 << bits) - 1
 
 
 def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cells: int, dev):
@@ -163,9 +185,15 @@ def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cells: int, dev):
 
 
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
-                     sh_rest=None, sh_degree=0, pair_counts=None):
+                     sh_rest=None, sh_degree=0, pair_counts=None, depth_window_ok=True):
     """pair_counts: optional int32 [H*W] the blend fills with each pixel's
-    contributing pairs (a measurement counter; not in render())."""
+    contributing pairs (a measurement counter; not in render()).
+
+    The depth sort runs over a window of the depth keys' bits chosen from the
+    previous frame's visible depth range on this device (one radix pass less
+    per 8 bits, gs_project_args.key_base); this frame's range, read back with
+    (M, T), says whether the window held -- if not, the frame is rendered
+    again with full 32-bit keys (depth_window_ok=False)."""
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -184,10 +212,13 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     keys = torch.empty((2, n), dtype=i32, device=dev)
     vals = torch.empty((2, n), dtype=i32, device=dev)
     counters = torch.empty((N.GS_NUM_COUNTERS,), dtype=i32, device=dev)
+    key_minmax = torch.empty((2 * max(1, (n + 255) // 256),), dtype=i32, device=dev)
+    window = _DEPTH_WINDOW.get(dev) if depth_window_ok else None
+    key_base, key_bits = window if window is not None else (0, 32)
 
     StageTimer.mark("project_fwd")
     pa = N.GsProjectArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(radii), N.ptr(vis), N.ptr(records),
-                         N.ptr(rects), N.ptr(keys[0]))
+                         N.ptr(rects), N.ptr(keys[0]), key_base, key_bits, N.ptr(key_minmax))
     N.check(lib.gs_project_forward(C.byref(pa), s), "gs_project_forward")
 
     fr = _Frame()
@@ -196,14 +227,15 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         ws = torch.empty((lib.gs_radix_sort_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         StageTimer.mark("depth_sort")
         alt = C.c_int32(0)
-        N.check(lib.gs_radix_sort_pairs(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n, 0, 32, 1,
-                                        N.ptr(ws), ws.numel(), C.byref(alt), s), "depth sort")
+        N.check(lib.gs_radix_sort_pairs(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n, 0,
+                                        key_bits, 1, N.ptr(ws), ws.numel(), C.byref(alt), s), "depth sort")
         sorted_ids = vals[alt.value]
         fr.order = sorted_ids
         bws = torch.empty((lib.gs_bin_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         pair_offset = torch.empty((n,), dtype=i32, device=dev)
         ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(vis),
-                         N.ptr(counters), N.ptr(bws), bws.numel(), 0, 0, N.ptr(pair_offset), N.ptr(records), 0)
+                         N.ptr(counters), N.ptr(key_minmax), N.ptr(bws), bws.numel(), 0, 0, N.ptr(pair_offset),
+                         N.ptr(records), 0)
         StageTimer.mark("bin_count")
         N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
         # everything whose size does not depend on T is allocated before the
@@ -225,8 +257,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         # is queued, so the host wakes while the GPU still emits
         host = _HOST_COUNTERS.get(dev)
         if host is None:
-            host = _HOST_COUNTERS[dev] = torch.empty((2,), dtype=i32, pin_memory=True)
-        host.copy_(counters[:2], non_blocking=True)
+            host = _HOST_COUNTERS[dev] = torch.empty((4,), dtype=i32, pin_memory=True)
+        host.copy_(counters[:4], non_blocking=True)
         ready = torch.cuda.Event()
         ready.record()
         if big_guess is not None:
@@ -236,8 +268,13 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
             N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
         StageTimer.mark("~sync")
         ready.synchronize()  # the one host sync
-        M, T = (int(v) for v in host.tolist())
+        M, T, zmin, zmax = (int(v) & 0xFFFFFFFF if i >= 2 else int(v) for i, v in enumerate(host.tolist()))
         _T_SEEN[dev] = T
+        _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
+        if not window_holds(window, zmin, zmax):
+            # a visible depth outside the window: the sort's keys were clipped
+            return forward_pipeline(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit,
+                                    sh_rest, sh_degree, pair_counts, depth_window_ok=False)
     else:
         M, T = 0, 0
     fr.M, fr.T = M, T

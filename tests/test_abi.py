@@ -60,6 +60,7 @@ def test_bad_arguments_are_reported(pkg):
     assert lib.gs_radix_sort_pairs(None, None, None, None, 10, 0, 40, 0, None, 0, C.byref(alt), None) == 1
     a = N.GsProjectArgs()
     a.cam.image_width = a.cam.image_height = 8
+    a.key_bits = 32
     for bad in (0, -4, 257):  # tile_size outside [1, GS_MAX_TILE]
         a.cam.tile_size = bad
         assert lib.gs_project_forward(C.byref(a), None) == 3
@@ -81,6 +82,10 @@ def test_bad_arguments_are_reported(pkg):
     assert lib.gs_project_forward(C.byref(a), None) == 3
     a.cam.radius_max, a.cam.radius_min = 1.0, 2.0
     assert lib.gs_project_forward(C.byref(a), None) == 3
+    a.cam.radius_min = 0.01
+    for bad in (0, 33):  # depth-key window bits
+        a.key_bits = bad
+        assert lib.gs_project_forward(C.byref(a), None) == 1
 
 
 def test_loss_bad_arguments(pkg):

@@ -467,3 +467,39 @@ def test_grad_bucket_adoption(pkg, cuda):
                 assert p.grad.data_ptr() == v.data_ptr()
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_depth_window_miss_rerenders(pkg, cuda):
+    """The depth sort runs over a window of key bits chosen from the previous
+    frame's visible depth range (rasterizer.depth_window); a frame whose depths
+    leave the window is rendered again with 32-bit keys.  Both a held window
+    and a missed one give the frame a fresh renderer gives, bit for bit."""
+    RZ = pkg.rasterizer
+    syn = pkg.synthetic
+    W, H = 320, 240
+    narrow = syn.make_scene(20000, W, H, seed=41, z_range=(2.0, 2.5))
+    wide = syn.make_scene(20000, W, H, seed=42, z_range=(0.5, 60.0))
+
+    def frame(sc):
+        m = syn.to_model(sc, pkg.GaussianModel, cuda)
+        out = pkg.GaussianRenderer().render(Cam(W, H, sc.fovx, sc.fovy), m, pkg.RenderSettings(H, W, torch.zeros(3)))
+        (out["image"].sum() + out["depth"].sum()).backward()
+        return out["image"].clone(), out["depth"].clone(), m._xyz.grad.clone(), m._scaling.grad.clone()
+
+    RZ._DEPTH_WINDOW.pop(cuda, None)
+    fresh_wide = frame(wide)             # 32-bit keys (no window yet)
+    frame(narrow)                        # leaves a narrow window behind
+    assert RZ._DEPTH_WINDOW[cuda] is not None and RZ._DEPTH_WINDOW[cuda][1] <= 24
+    missed = frame(wide)                 # leaves the window: re-rendered with 32-bit keys
+    held = frame(wide)                   # its own window now
+    assert RZ._DEPTH_WINDOW[cuda] is None or RZ._DEPTH_WINDOW[cuda][1] > 16
+    frame(narrow)
+    held_narrow = frame(narrow)
+    RZ._DEPTH_WINDOW.pop(cuda, None)
+    fresh_narrow = frame(narrow)
+    for a, b in zip(fresh_wide, missed):
+        assert torch.equal(a, b)
+    for a, b in zip(fresh_wide, held):
+        assert torch.equal(a, b)
+    for a, b in zip(fresh_narrow, held_narrow):
+        assert torch.equal(a, b)

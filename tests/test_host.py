@@ -107,3 +107,21 @@ def test_synthetic_scene_distribution(pkg):
     assert torch.allclose(sc.rotation.norm(dim=1), torch.ones(5000), atol=1e-5)
     sc2 = pkg.synthetic.make_scene(5000, 192, 108, seed=0)
     assert torch.equal(sc.xyz, sc2.xyz)
+
+
+def test_depth_window_choice(pkg):
+    """rasterizer.depth_window: a window of key bits around the previous
+    frame's visible fp32 depth bits, widened by 1/8 of the range each side;
+    None when it would not save a radix pass."""
+    import struct
+    RZ = pkg.rasterizer
+    bits = lambda z: struct.unpack("<I", struct.pack("<f", z))[0]
+    w = RZ.depth_window(bits(2.0), bits(6.0))  # the C3 distribution: 24 bits, 3 passes
+    assert w is not None and w[1] <= 24
+    assert RZ.window_holds(w, bits(2.0), bits(6.0)) and RZ.window_holds(w, bits(2.1), bits(5.5))
+    assert not RZ.window_holds(w, bits(0.5), bits(6.0)) and not RZ.window_holds(w, bits(2.0), bits(60.0))
+    assert RZ.depth_window(bits(0.01), bits(1000.0)) is None  # > 24 bits: no pass saved
+    assert RZ.depth_window(0xFFFFFFFF, 0) is None  # nothing visible
+    assert RZ.window_holds(None, bits(0.01), bits(1e30))
+    base, nb = RZ.depth_window(bits(3.0), bits(3.0))  # a single depth
+    assert nb >= 1 and RZ.window_holds((base, nb), bits(3.0), bits(3.0))

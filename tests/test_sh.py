@@ -53,8 +53,9 @@ def test_sh_degree_is_validated(pkg):
     fake = C.c_void_p(16)
     for f in ("xyz", "color_logits", "opacity", "cov3d"):
         setattr(a.g, f, fake)
-    for f in ("means2d", "conics", "radii", "vis", "records", "rects", "depth_keys"):
+    for f in ("means2d", "conics", "radii", "vis", "records", "rects", "depth_keys", "key_minmax"):
         setattr(a, f, fake)
+    a.key_bits = 32
     a.g.sh_degree = 4
     assert lib.gs_project_forward(C.byref(a), None) == 1
     assert b"sh_degree" in lib.gs_last_error()
