@@ -30,7 +30,7 @@ constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
 constexpr int kSortIpt = 8;                      // items per thread per sort block
 constexpr int kSortChunk = kBlock * kSortIpt;    // 2048 items per block
-constexpr int kBinChunk = kBlock * 4;            // 1024 Gaussians per binning block
+constexpr int kBinChunk = kBlock * 4;            // 1024 Gaussians per binning block (2 and 1 rounds: slower)
 constexpr float kAlphaStop = 0.995f;             // renderer.py:352
 // renderer.py:336 skips a pair when w = exp(-s/2) < 1e-5; decided here on
 // s: s > 2 ln(1e5).  The same decision except where exp's rounding

@@ -197,8 +197,13 @@ def test_radix_sort_matches_stable_argsort(pkg, cuda):
     N = pkg._native
     lib = N.load()
     rng = np.random.default_rng(3)
-    for n, bits in ((1, 8), (1000, 13), (123457, 32), (70000, 4)):
+    # (n, bits, top): top = a constant top byte (depth keys with z in [2, 4):
+    # the last of four 8-bit passes sees one digit only), 24 = a depth window
+    for n, bits, top in ((1, 8, None), (1000, 13, None), (123457, 32, None), (70000, 4, None),
+                         (50000, 32, 0x40), (100000, 24, None), (4099, 20, None)):
         k = rng.integers(0, 1 << min(bits, 31), n, dtype=np.int64).astype(np.uint32)
+        if top is not None:
+            k = (k & 0x00FFFFFF) | np.uint32(top << 24)
         if bits == 32:
             k[::7] = 0xFFFFFFFF
         keys = torch.tensor(k.view(np.int32), device=cuda)
