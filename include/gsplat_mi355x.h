@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 8
+#define GS_ABI_VERSION 9
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
@@ -44,7 +44,7 @@ extern "C" {
                                  gs_project_forward returns GS_ERR_UNSUPPORTED otherwise */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian, 8x8 cell) gradient partial */
-#define GS_PARTIAL_STRIDE 12   /* floats between partials in pair_grads (10 used; 16-B aligned) */
+#define GS_PARTIAL_STRIDE 10   /* floats between partials in pair_grads (dense: 40 B each) */
 #define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2] / [3] min / max fp32 bits of the
                                  visible depths (0xFFFFFFFF / 0 when none; see gs_project_args) */
 

@@ -25,9 +25,9 @@ GS_MAX_TILE = 256
 GS_QUAD = 8  # 8x8 pixel cells per wave, ceil(tile/8)^2 per tile (gs_tile_quads)
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
-GS_PARTIAL_STRIDE = 12  # floats between quadrant partials in pair_grads
+GS_PARTIAL_STRIDE = 10  # floats between cell partials in pair_grads (dense)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 8
+GS_ABI_VERSION = 9
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p

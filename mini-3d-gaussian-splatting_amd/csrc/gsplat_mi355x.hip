@@ -1375,9 +1375,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
   for (uint32_t qc = (uint32_t)q; cnt > (uint32_t)h && qc < ncell; qc += 4) {
     const size_t off = off32;
     const uint8_t *flag = a.slot_live + off * ncell + qc;  // (slot e, cell qc) at flag[Q e]
-    // cell-qc partial of slot e at part[e * Q * kS4] (48-B records: 16-B loads)
-    constexpr int kS4 = GS_PARTIAL_STRIDE / 4;
-    const float4 *part = reinterpret_cast<const float4 *>(a.pair_grads + (off * ncell + qc) * GS_PARTIAL_STRIDE);
+    // cell-qc partial of slot e at part + e * Q * GS_PARTIAL_STRIDE (dense 40-B
+    // records, 8-B aligned: global loads need 4-B alignment only)
+    const float *part = a.pair_grads + (off * ncell + qc) * GS_PARTIAL_STRIDE;
     for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += 8) {
       // the 4 flags in one round trip: unconditional loads (past the end
       // the clamped index re-reads slot e0), masked after
@@ -1400,7 +1400,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
       float2 vc[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float4 *src = part + (size_t)(e0 + 2 * i) * ncell * kS4;
+        const float4 *src = reinterpret_cast<const float4 *>(part + (size_t)(e0 + 2 * i) * ncell * GS_PARTIAL_STRIDE);
         va[i] = f[i] ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
         vb[i] = f[i] ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
         vc[i] = f[i] ? *reinterpret_cast<const float2 *>(src + 2) : make_float2(0.f, 0.f);
