@@ -15,7 +15,11 @@ Gaussians and hands each finished range to rows_ready(), which issues its
 all-reduces asynchronously (RCCL's own stream waits for the range's kernels
 only): range k's reduction runs while range k+1 is computed.
 all_reduce_mean() then waits for them.  Every rank issues the same ranges in
-the same order (same N, same chunk rule), as collectives must match.
+the same order (same N, same chunk rule), as collectives must match.  The
+default is one range (one all_reduce call over the whole bucket, issued the
+moment the backward's last kernel is queued): a range below the whole costs
+one call per parameter slice, ~25-30 us of host time each on the box, more
+than the ~70 us of gather + projection backward a second range can hide.
 """
 from __future__ import annotations
 
@@ -45,7 +49,10 @@ class GradAllReduce:
         self._sizes: List[int] = []
         # overlap ranges: `chunks` when every range keeps >= min_chunk_rows
         # Gaussians (smaller launches would not fill the GPU)
-        self.chunks = int(chunks if chunks is not None else os.environ.get("GS_ALLREDUCE_CHUNKS", 2))
+        # default 1: measured on the box (RCCL, world size 1), every all_reduce call
+        # costs ~25-30 us of host time the GPU then waits for; with one range the
+        # whole bucket goes in one call, issued as soon as the backward is queued
+        self.chunks = int(chunks if chunks is not None else os.environ.get("GS_ALLREDUCE_CHUNKS", 1))
         self.min_chunk_rows = int(min_chunk_rows if min_chunk_rows is not None
                                   else os.environ.get("GS_ALLREDUCE_MIN_ROWS", 1 << 16))
         self._works: list = []
@@ -84,6 +91,9 @@ class GradAllReduce:
         n = self.params[0].shape[0]
         op = self.dist.ReduceOp.AVG if self._avg else self.dist.ReduceOp.SUM
         self.ranges_reduced += 1
+        if lo == 0 and hi == n:  # every row: the whole bucket in one call
+            self._works.append(self.dist.all_reduce(flat, op=op, group=self.group, async_op=True))
+            return
         off = 0
         for size in self._sizes:
             cols = size // n

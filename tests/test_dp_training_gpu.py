@@ -62,8 +62,8 @@ def test_dp_trainer_two_ranks_match_mean_of_views(pkg, cuda, tmp_path, overlap):
     write_scene_files(tmp_path)
     port = _free_port()
     outs = [tmp_path / f"rank{r}.npz" for r in range(2)]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", GS_ALLREDUCE_CHUNKS="2",
-               GS_ALLREDUCE_MIN_ROWS="256" if overlap else str(1 << 30))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", GS_ALLREDUCE_CHUNKS="2" if overlap else "1",
+               GS_ALLREDUCE_MIN_ROWS="256")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), str(r), "2", str(port),
                                str(tmp_path), str(outs[r])], env=env) for r in range(2)]
     try:

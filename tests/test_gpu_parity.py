@@ -455,7 +455,7 @@ def test_grad_bucket_adoption(pkg, cuda):
         m = syn.to_model(sc, pkg.GaussianModel, cuda)
         params = m.grad_parameters()
         stub = _OneRankDist()
-        red = pkg.distributed.GradAllReduce(params, dist=stub, min_chunk_rows=4096)
+        red = pkg.distributed.GradAllReduce(params, dist=stub, chunks=2, min_chunk_rows=4096)
         if attach:
             red.attach(m)
         out = pkg.GaussianRenderer().render(Cam(320, 240, sc.fovx, sc.fovy), m,
@@ -464,6 +464,8 @@ def test_grad_bucket_adoption(pkg, cuda):
         if attach:
             # the backward handed its rows over in two ranges, one slice per parameter each
             assert red.ranges_reduced == 2 and len(stub.sliced) == 2 * len(params)
+            red2 = pkg.distributed.GradAllReduce(params, dist=_OneRankDist())
+            assert red2.overlap_chunks() == 1  # the default: the whole bucket in one call
             assert sum(stub.sliced) == sum(p.numel() for p in params)
             red.all_reduce_mean()
         res.append([p.grad.clone() for p in params])
