@@ -394,12 +394,13 @@ def test_c2_full_size_vs_oracle(pkg, cuda):
     assert not errs, errs
 
 
-@pytest.mark.parametrize("tile", [4, 8, 20, 32])
+@pytest.mark.parametrize("tile", [1, 3, 4, 8, 20, 32, 64])
 def test_tile_sizes_vs_oracle(pkg, cuda, tile):
     """GaussianRenderer(tile_size=L): every pixel blends its L x L tile's list
     (renderer.py:261-311), so L changes the image.  Partial edge tiles,
-    cells clipped to tiles (L = 4, 20), several cell groups per tile (32)."""
-    W, H = 200, 152
+    cells clipped to tiles (L = 1, 3, 4, 20: one pixel per tile up to cells
+    partly outside it), several cells per tile (32, 64)."""
+    W, H = (200, 152) if tile >= 4 else (72, 56)
     sc = pkg.synthetic.make_scene(3000, W, H, seed=20 + tile, sigma_range=(0.01, 0.05))
     errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.1, 0.0, 0.3), renderer_kw=dict(tile_size=tile),
                                     label=f"tile{tile}")
@@ -510,3 +511,16 @@ def test_depth_window_miss_rerenders(pkg, cuda):
         assert torch.equal(a, b)
     for a, b in zip(fresh_narrow, held_narrow):
         assert torch.equal(a, b)
+
+
+def test_no_gaussians(pkg, cuda):
+    """N = 0 (an empty model): the early return of renderer.py:74-83 (bg once,
+    zero alpha and depth) and empty gradients."""
+    g = Gauss(np.zeros((0, 3)), np.zeros((0, 3, 3)), np.zeros((0, 3)), np.zeros(0), cuda)
+    out = pkg.GaussianRenderer().render(Cam(32, 24, np.radians(60), np.radians(50)), g,
+                                        pkg.RenderSettings(24, 32, torch.tensor([0.2, 0.3, 0.4])))
+    assert torch.allclose(out["image"].cpu(), torch.tensor([0.2, 0.3, 0.4]).view(3, 1, 1).expand(3, 24, 32))
+    assert out["alpha"].abs().sum() == 0 and out["depth"].abs().sum() == 0
+    assert out["viewspace_points"].shape == (0, 2) and out["radii"].shape == (0,)
+    out["viewspace_points"].sum().backward()
+    assert g.xyz.grad is not None and g.xyz.grad.shape == (0, 3)
