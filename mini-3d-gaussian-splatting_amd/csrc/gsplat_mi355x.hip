@@ -453,25 +453,35 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restric
     if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(m));
   }
   __syncthreads();
-  counts[(size_t)threadIdx.x * nb + blockIdx.x] = hist[threadIdx.x];
+  if (threadIdx.x <= mask) counts[(size_t)threadIdx.x * nb + blockIdx.x] = hist[threadIdx.x];
 }
 
 // row d of counts -> exclusive prefix over blocks; totals[d] = row sum.
+// Thread t owns a contiguous run of `per` (<= kScanPer) entries of each
+// 256 * per stretch (loads all in flight): one block scan per stretch (nb <=
+// 4096, 8.4M keys: one) instead of one per 256 entries.
+constexpr int kScanPer = 16;
 __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, uint32_t *totals, int nb) {
   __shared__ uint32_t s_tmp[4];
   const int d = blockIdx.x;
   uint32_t *row = counts + (size_t)d * nb;
+  const int per = min(kScanPer, (nb + kBlock - 1) / kBlock);
   uint32_t carry = 0, tot;
-  // the next chunk's load in flight during this chunk's scan (unconditional,
-  // clamped index: no branch for the compiler to wait at)
-  uint32_t vn = row[(int)threadIdx.x < nb ? (int)threadIdx.x : nb - 1];
-  for (int c = 0; c < nb; c += kBlock) {
-    const int i = c + threadIdx.x;
-    const uint32_t v = i < nb ? vn : 0u;
-    const int inext = i + kBlock;
-    vn = row[inext < nb ? inext : nb - 1];
-    const uint32_t e = block_exscan(v, s_tmp, &tot);
-    if (i < nb) row[i] = carry + e;
+  for (int c = 0; c < nb; c += kBlock * per) {
+    const int i0 = c + (int)threadIdx.x * per;
+    uint32_t v[kScanPer];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      v[k] = (k < per && i0 + k < nb) ? row[i0 + k] : 0u;
+      sum += v[k];
+    }
+    uint32_t run = carry + block_exscan(sum, s_tmp, &tot);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      if (k < per && i0 + k < nb) row[i0 + k] = run;
+      run += v[k];
+    }
     carry += tot;
   }
   if (threadIdx.x == 0) totals[d] = carry;
@@ -505,9 +515,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
     k_[r] = keys_in[ci];
     v_[r] = kIota ? (uint32_t)idx : vals_in[ci];
   }
-  const uint32_t my_prefix = counts[(size_t)threadIdx.x * nb + blockIdx.x];  // (also in flight)
+  // (also in flight; rows and totals exist for the pass's 2^nbits digits only)
+  const bool dig = threadIdx.x <= mask;
+  const uint32_t my_prefix = dig ? counts[(size_t)threadIdx.x * nb + blockIdx.x] : 0u;
   uint32_t tot;
-  const uint32_t dbase = block_exscan(totals[threadIdx.x], s_tmp, &tot);  // includes a barrier
+  const uint32_t dbase = block_exscan(dig ? totals[threadIdx.x] : 0u, s_tmp, &tot);  // includes a barrier
   uint32_t rk[kSortIpt];
 #pragma unroll
   for (int r = 0; r < kSortIpt; ++r) {
@@ -906,6 +918,12 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
   // tile or image start done
   float A = inside ? 0.f : 1.f, D = 0.f;
   uint32_t neval = 0, ncontrib = 0;
+  // neval (1 + the last entry this lane evaluated while running, :352) is
+  // kept lazily: `last` is that count for the running lanes of the last
+  // evaluated entry (scalar), copied into a lane's neval only when it stops
+  // (its bit leaves the running mask) -- two VALU less per evaluated entry
+  uint32_t last = 0;
+  unsigned long long runm = __builtin_amdgcn_ballot_w64(A < kAlphaStop);
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   // liveness word of (this batch, this cell): see gs_blend_live_words
@@ -948,9 +966,16 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
       const float dx = fx - pm.x, dy = fy - pm.y;
       const float s = conic_s(dx, dy, pq.x, po.x, pq.y);  // :333
       const bool run = A < kAlphaStop;
+      const unsigned long long rm = __builtin_amdgcn_ballot_w64(run);  // (the compare's own SGPR result)
       const bool lv = run && !(s > kSkipS);  // the :336 skip, decided on s
       if (wave_any(lv)) {
         livem |= 1ull << bit;
+        if (rm != runm) {  // lanes stopped since the last evaluated entry (rare)
+          asm volatile("" ::: "memory");  // a real branch: not if-converted into every entry
+          if ((runm >> lane) & 1ull) neval = last;
+          runm = rm;
+        }
+        last = b - start + bit + 1;
         const float w = sat01(exp_neg_half(s));          // :334
         const float ai = lv ? sat01(po.y * w) : 0.f;      // :339 (skips folded into the weight)
         const float c = (1.f - A) * ai;                   // :343-344
@@ -961,13 +986,13 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
         A = A + c;
         D = __builtin_fmaf(c, pbz.y, D);
         if constexpr (kCount) ncontrib += c > 0.f ? 1u : 0u;
-        neval = run ? b - start + bit + 1 : neval;  // :352, see k_blend_fwd
       }
     }
     const uint64_t wi = (b - start) / 64u;
     if (lane == 0 && wi < live_left) live[wi] = livem;
   }
   if (!inside) return;
+  if ((runm >> lane) & 1ull) neval = last;
   if (A < kAlphaStop) neval = end - start;
   const size_t HW = (size_t)W * H, p = (size_t)py * W + px;
   const float tb = 1.f - A;
@@ -1827,7 +1852,7 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
   for (int p = 0; p < passes; ++p) {
     const int nbits = (end_bit - shift + (passes - p) - 1) / (passes - p);
     k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, nb);
-    k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, totals, nb);
+    k_radix_scan<<<1 << nbits, kBlock, 0, s>>>(counts, totals, nb);
     if (p == 0 && vals_are_iota)
       k_radix_scatter<true><<<nb, kBlock, 0, s>>>(kin, nullptr, kout, vout, n, shift, nbits, counts, totals, nb);
     else

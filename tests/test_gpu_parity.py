@@ -199,8 +199,13 @@ def test_radix_sort_matches_stable_argsort(pkg, cuda):
     rng = np.random.default_rng(3)
     # (n, bits, top): top = a constant top byte (depth keys with z in [2, 4):
     # the last of four 8-bit passes sees one digit only), 24 = a depth window
-    for n, bits, top in ((1, 8, None), (1000, 13, None), (123457, 32, None), (70000, 4, None),
-                         (50000, 32, 0x40), (100000, 24, None), (4099, 20, None)):
+    # (4.5M, 13): a C3-sized tile sort; (.., 8, 20): a bit range not starting
+    # at 0; iota = 0: caller-given values.  The workspace is refilled with
+    # garbage before every call (the look-back status must be cleared by the sort).
+    for n, bits, top, lo, iota in ((1, 8, None, 0, 1), (1000, 13, None, 0, 1), (123457, 32, None, 0, 1),
+                                   (70000, 4, None, 0, 1), (50000, 32, 0x40, 0, 1), (100000, 24, None, 0, 1),
+                                   (4099, 20, None, 0, 1), (4_500_000, 13, None, 0, 0), (30000, 20, None, 8, 0),
+                                   (2048, 16, None, 0, 0), (2049, 16, None, 0, 1)):
         k = rng.integers(0, 1 << min(bits, 31), n, dtype=np.int64).astype(np.uint32)
         if top is not None:
             k = (k & 0x00FFFFFF) | np.uint32(top << 24)
@@ -210,14 +215,19 @@ def test_radix_sort_matches_stable_argsort(pkg, cuda):
         kk = torch.empty((2, n), dtype=torch.int32, device=cuda)
         vv = torch.empty((2, n), dtype=torch.int32, device=cuda)
         kk[0].copy_(keys)
-        ws = torch.empty(lib.gs_radix_sort_workspace_bytes(n), dtype=torch.uint8, device=cuda)
+        v0 = rng.permutation(n).astype(np.uint32)
+        if not iota:
+            vv[0].copy_(torch.tensor(v0.view(np.int32)))
+        ws = torch.full((lib.gs_radix_sort_workspace_bytes(n),), 0xAB, dtype=torch.uint8, device=cuda)
         alt = C.c_int32(0)
-        N.check(lib.gs_radix_sort_pairs(N.ptr(kk[0]), N.ptr(vv[0]), N.ptr(kk[1]), N.ptr(vv[1]), n, 0, bits, 1,
+        N.check(lib.gs_radix_sort_pairs(N.ptr(kk[0]), N.ptr(vv[0]), N.ptr(kk[1]), N.ptr(vv[1]), n, lo, bits, iota,
                                         N.ptr(ws), ws.numel(), C.byref(alt), torch.cuda.current_stream().cuda_stream),
                 "sort")
-        order = np.argsort(k, kind="stable")
-        assert np.array_equal(vv[alt.value].cpu().numpy().view(np.uint32), order.astype(np.uint32))
-        assert np.array_equal(kk[alt.value].cpu().numpy().view(np.uint32), k[order])
+        digit = (k >> np.uint32(lo)) & np.uint32((1 << (bits - lo)) - 1) if bits - lo < 32 else k
+        order = np.argsort(digit, kind="stable")
+        want_v = order.astype(np.uint32) if iota else v0[order]
+        assert np.array_equal(vv[alt.value].cpu().numpy().view(np.uint32), want_v), (n, bits, lo, iota)
+        assert np.array_equal(kk[alt.value].cpu().numpy().view(np.uint32), k[order]), (n, bits, lo, iota)
 
 
 def test_tile_ranges_every_tile(pkg, cuda):
