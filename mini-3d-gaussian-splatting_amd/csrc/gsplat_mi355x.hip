@@ -576,7 +576,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
 }
 
 // ======================================================== binning =========
-// partials[0..nb): touches per block, partials[nb..2nb): visible per block,
+// partials[0..nb): touches per block (depth order), partials[nb..2nb): visible per index chunk,
 // [2nb..3nb): index-order slots per chunk, [3nb..5nb): depth-bits min / max per chunk
 __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials, int nb) {
   __shared__ uint32_t s_tmp[4];
@@ -597,11 +597,12 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
   }
   uint32_t sum = 0, nvis = 0;
   uint2 rc_d[kR];
-  uint32_t vis_d[kR];
+  uint32_t vis_o[kR];
 #pragma unroll
   for (int i = 0; i < kR; ++i) {
+    const long long k = base + i * kBlock + threadIdx.x;
     rc_d[i] = reinterpret_cast<const uint2 *>(a.rects)[gi[i]];
-    vis_d[i] = a.vis[gi[i]];
+    vis_o[i] = a.vis[k < a.n ? k : a.n - 1];  // M is a total: counted in index order (coalesced)
   }
 #pragma unroll
   for (int i = 0; i < kR; ++i) {
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
     if (k < a.n) {
       sum += rect_touches((int)(rc_d[i].x & 0xFFFFu), (int)(rc_d[i].x >> 16), (int)(rc_d[i].y & 0xFFFFu),
                           (int)(rc_d[i].y >> 16));
-      nvis += vis_d[i] ? 1u : 0u;
+      nvis += vis_o[i] ? 1u : 0u;
     }
   }
   uint32_t tot, totv;

@@ -431,6 +431,26 @@ def test_wide_rects_vs_oracle(pkg, cuda):
     assert not errs, errs
 
 
+@pytest.mark.parametrize("wh", [(1, 1), (5, 3), (17, 1), (1, 33), (129, 65)])
+def test_odd_image_sizes_vs_oracle(pkg, cuda, wh):
+    """Images of one pixel, one row, one column, and sizes just past a tile
+    multiple: every cell of a tile but one is outside the image."""
+    W, H = wh
+    sc = pkg.synthetic.make_scene(400, W, H, seed=40 + W + H, sigma_range=(0.01, 0.2))
+    errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.2, 0.1, 0.0), label=f"{W}x{H}")
+    assert bad.sum() <= 1
+    assert not errs, errs
+
+
+def test_4k_frame_vs_oracle(pkg, cuda):
+    """3840x2160 (32,400 tiles: 15-bit tile keys), fwd + bwd vs the oracle."""
+    W, H = 3840, 2160
+    sc = pkg.synthetic.make_scene(60_000, W, H, seed=9)
+    errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.0, 0.0, 0.0), label="4K")
+    assert bad.sum() <= 16
+    assert not errs, errs
+
+
 class _OneRankDist:
     """torch.distributed stand-in for one rank: all_reduce is the identity,
     slices handed to it are recorded."""
