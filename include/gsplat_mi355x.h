@@ -173,7 +173,9 @@ typedef struct gs_bin_args {
   const uint8_t *vis;         /* [n]   from gs_project_forward */
   uint32_t *counters;         /* [GS_NUM_COUNTERS] */
   const uint32_t *key_minmax; /* gs_project_args.key_minmax (reduced into counters[2..3]) */
-  void *workspace;
+  void *workspace;             /* gs_bin_workspace_bytes(n); gs_bin_count leaves the per-block
+                                  partials and the depth-ordered rectangles there for gs_bin_emit:
+                                  pass the same workspace to both, untouched in between */
   size_t workspace_bytes;
   /* emit outputs (tile_keys / pair_gauss / records ignored by gs_bin_count) */
   uint32_t *tile_keys;   /* [T] */

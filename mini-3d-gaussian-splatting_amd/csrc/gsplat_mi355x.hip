@@ -576,6 +576,12 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
 }
 
 // ======================================================== binning =========
+// The binning workspace: 5 nb words of per-block partials, then the
+// depth-ordered rectangles (n uint2, 16-B aligned).
+__device__ __forceinline__ uint2 *sorted_rects(uint32_t *partials, int nb) {
+  return reinterpret_cast<uint2 *>(partials + ((5 * nb + 3) & ~3));
+}
+
 // partials[0..nb): touches per block (depth order), partials[nb..2nb): visible per index chunk,
 // [2nb..3nb): index-order slots per chunk, [3nb..5nb): depth-bits min / max per chunk
 __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials, int nb) {
@@ -619,6 +625,13 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
   if (threadIdx.x == 0) {
     partials[blockIdx.x] = tot;
     partials[nb + blockIdx.x] = totv;
+  }
+  // the depth-ordered rectangles, for k_bin_emit to read coalesced
+  uint2 *srect = sorted_rects(partials, nb);
+#pragma unroll
+  for (int i = 0; i < kR; ++i) {
+    const long long k = base + i * kBlock + threadIdx.x;
+    if (k < a.n) srect[k] = rc_d[i];
   }
   // Gradient slots are numbered in Gaussian-index order (a Gaussian's
   // touches consecutive), so that gs_project_backward's threads g, g+1 read
@@ -735,19 +748,20 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   const long long base = (long long)blockIdx.x * kBinChunk;
   uint32_t out_base = partials[blockIdx.x];
   constexpr int kR = kBinChunk / kBlock;
-  // all rounds' ids, then their rects, unconditionally (clamped): two round
-  // trips for the block instead of two per round
+  // all rounds' ids and rects unconditionally (clamped): one round trip for
+  // the block
   uint32_t gr[kR];
   uint2 rcr[kR];
   uint32_t offr[kR];
+  const uint2 *srect = sorted_rects(const_cast<uint32_t *>(partials), (int)gridDim.x);
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     const long long k = base + r * kBlock + threadIdx.x;
-    gr[r] = a.sorted_ids[k < a.n ? k : a.n - 1];
-    offr[r] = a.pair_offset[k < a.n ? k : a.n - 1];  // (index order, for the slot pass below)
+    const long long kc = k < a.n ? k : a.n - 1;
+    gr[r] = a.sorted_ids[kc];
+    rcr[r] = srect[kc];  // (k_bin_partials' depth-ordered copy: no gather by id)
+    offr[r] = a.pair_offset[kc];  // (index order, for the slot pass below)
   }
-#pragma unroll
-  for (int r = 0; r < kR; ++r) rcr[r] = reinterpret_cast<const uint2 *>(a.rects)[gr[r]];
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     const long long k = base + r * kBlock + threadIdx.x;
@@ -1871,7 +1885,8 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
 }
 
 size_t gs_bin_workspace_bytes(int32_t n) {
-  return 5 * sizeof(uint32_t) * (size_t)(n > 0 ? div_up(n, kBinChunk) : 1) + 256;
+  const size_t nb = n > 0 ? div_up(n, kBinChunk) : 1;
+  return sizeof(uint32_t) * ((5 * nb + 3) & ~(size_t)3) + sizeof(uint32_t) * 2 * (size_t)(n > 0 ? n : 0) + 256;
 }
 
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
@@ -1894,6 +1909,8 @@ gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream) {
   if (!a->sorted_ids || !a->rects || !a->counters || !a->workspace || !a->tile_keys || !a->pair_gauss ||
       !a->pair_offset || !a->records)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_bin_emit");
+  if (a->workspace_bytes < gs_bin_workspace_bytes(a->n))
+    return fail(GS_ERR_INVALID_ARG, "%s: workspace too small", "gs_bin_emit");
   if (a->capacity < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative capacity", "gs_bin_emit");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
