@@ -28,7 +28,10 @@ constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
-constexpr int kSortIpt = 8;                      // items per thread per sort block
+#ifndef GS_SORT_IPT
+#define GS_SORT_IPT 8
+#endif
+constexpr int kSortIpt = GS_SORT_IPT;            // items per thread per sort block
 constexpr int kSortChunk = kBlock * kSortIpt;    // 2048 items per block
 constexpr int kBinChunk = kBlock * 4;            // 1024 Gaussians per binning block (2 and 1 rounds: slower)
 constexpr float kAlphaStop = 0.995f;             // renderer.py:352
