@@ -37,9 +37,20 @@ def _worker(rank, world, port, q):
         local = [None if p.grad is None else p.grad.clone() for p in params]
         red = pkg.distributed.GradAllReduce(params, dist)
         red.all_reduce_mean()
-        q.put((rank, local, [p.grad.clone() for p in params]))
+        q.put(_by_value(rank, local, [p.grad.clone() for p in params]))
     finally:
         dist.destroy_process_group()
+
+
+def _by_value(rank, local, reduced):
+    """Queue payload as numpy copies: torch tensors would travel as shared-memory
+    handles that vanish when the worker exits before the parent has read them."""
+    npy = lambda ts: [None if t is None else t.detach().numpy().copy() for t in ts]
+    return rank, npy(local), npy(reduced)
+
+
+def _from_value(ts):
+    return [None if a is None else torch.from_numpy(a) for a in ts]
 
 
 def test_grad_all_reduce_mean_gloo():
@@ -52,7 +63,7 @@ def test_grad_all_reduce_mean_gloo():
     res = dict()
     for _ in range(2):
         r, local, reduced = q.get(timeout=120)
-        res[r] = (local, reduced)
+        res[r] = (_from_value(local), _from_value(reduced))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -94,7 +105,7 @@ def _worker_zero_copy(rank, world, port, q, ranges=None):
             red.rows_ready(lo, hi)  # what the chunked backward does after each range
         red.all_reduce_mean()
         assert [p.grad.data_ptr() for p in params] == ptrs  # reduced in place, no copies
-        q.put((rank, local, [p.grad.clone() for p in params]))
+        q.put(_by_value(rank, local, [p.grad.clone() for p in params]))
     finally:
         dist.destroy_process_group()
 
@@ -114,7 +125,7 @@ def test_grad_all_reduce_zero_copy_gloo(ranges):
     res = dict()
     for _ in range(2):
         r, local, reduced = q.get(timeout=120)
-        res[r] = (local, reduced)
+        res[r] = (_from_value(local), _from_value(reduced))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
