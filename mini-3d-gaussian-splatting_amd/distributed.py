@@ -17,9 +17,12 @@ only): range k's reduction runs while range k+1 is computed.
 all_reduce_mean() then waits for them.  Every rank issues the same ranges in
 the same order (same N, same chunk rule), as collectives must match.  The
 default is one range (one all_reduce call over the whole bucket, issued the
-moment the backward's last kernel is queued): a range below the whole costs
-one call per parameter slice, ~25-30 us of host time each on the box, more
-than the ~70 us of gather + projection backward a second range can hide.
+moment the backward's last kernel is queued).  A range below the whole is
+one coalesced collective over its five parameter slices (RCCL group launch;
+five separate calls cost ~25-30 us of host time each): measured at world
+size 1, two ranges cost ~70 us more per step than one (four: ~160 us),
+about what a second range could hide behind the gather + projection backward
+at world 8, so one range stays the default (GS_ALLREDUCE_CHUNKS overrides).
 """
 from __future__ import annotations
 
@@ -56,6 +59,9 @@ class GradAllReduce:
         self.min_chunk_rows = int(min_chunk_rows if min_chunk_rows is not None
                                   else os.environ.get("GS_ALLREDUCE_MIN_ROWS", 1 << 16))
         self._works: list = []
+        # coalesced range reductions (torch's _coalescing_manager): RCCL only
+        self._coalesce = (os.environ.get("GS_ALLREDUCE_COALESCE", "1") != "0" and hasattr(dist, "is_initialized")
+                          and dist.is_initialized() and dist.get_backend(group) == "nccl")
         self.ranges_reduced = 0  # rows_ready calls so far (diagnostic)
         # RCCL (backend "nccl") forms the mean inside the reduction (ReduceOp.AVG,
         # NCCL >= 2.10); gloo has no AVG: SUM, then one division.  Decided once.
@@ -94,12 +100,22 @@ class GradAllReduce:
         if lo == 0 and hi == n:  # every row: the whole bucket in one call
             self._works.append(self.dist.all_reduce(flat, op=op, group=self.group, async_op=True))
             return
-        off = 0
+        # the range's slice of every parameter, coalesced into one collective
+        # (one RCCL group launch) where the backend supports it
+        slices, off = [], 0
         for size in self._sizes:
             cols = size // n
-            self._works.append(self.dist.all_reduce(flat[off + lo * cols: off + hi * cols], op=op,
-                                                    group=self.group, async_op=True))
+            slices.append(flat[off + lo * cols: off + hi * cols])
             off += size
+        cm_fn = getattr(self.dist, "_coalescing_manager", None)
+        if cm_fn is not None and self._coalesce:
+            with cm_fn(group=self.group, device=flat.device, async_ops=True) as cm:
+                for t in slices:
+                    self.dist.all_reduce(t, op=op, group=self.group)
+            self._works.append(cm)
+            return
+        for t in slices:
+            self._works.append(self.dist.all_reduce(t, op=op, group=self.group, async_op=True))
 
     def grad_destinations(self, leaves) -> Optional[List[torch.Tensor]]:
         """Bucket views shaped like `leaves`, when every leaf is one of this
