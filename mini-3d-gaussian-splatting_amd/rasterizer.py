@@ -184,6 +184,29 @@ def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cells: int, dev):
     return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
 
 
+class _TileLayout:
+    """Addresses inside one _alloc_tile_buffers allocation of capacity `cap`:
+    tile keys and Gaussian ids (ping-pong), the tile sort's workspace, the
+    liveness bitmap (stride live_words, sized for `cap` entries)."""
+    __slots__ = ("big", "cap", "p_tk", "p_tv", "p_ws", "ws_bytes", "o_live", "p_live", "live_words", "bits")
+
+
+def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
+    big, cap = buf
+    L = _TileLayout()
+    L.big, L.cap = big, cap
+    base = big.data_ptr()
+    L.p_tk = (base, base + 4 * cap)             # tile keys, ping-pong
+    L.p_tv = (base + 8 * cap, base + 12 * cap)  # Gaussian ids, ping-pong
+    o_ws = (16 * cap + 255) // 256 * 256
+    L.ws_bytes = int(lib.gs_radix_sort_workspace_bytes(cap))  # (>= what any T <= cap needs)
+    L.o_live = o_ws + (L.ws_bytes + 255) // 256 * 256
+    L.p_ws, L.p_live = base + o_ws, base + L.o_live
+    L.live_words = int(lib.gs_blend_live_words(cap, num_tiles))
+    L.bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
+    return L
+
+
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
                      sh_rest=None, sh_degree=0, pair_counts=None, depth_window_ok=True):
     """pair_counts: optional int32 [H*W] the blend fills with each pixel's
@@ -266,13 +289,16 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
             ba.tile_keys, ba.pair_gauss, ba.capacity = gb, gb + 8 * gcap, gcap
             StageTimer.mark("bin_emit")
             N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
+            # everything the launches after the sync need but T, laid out now
+            # (the GPU is emitting): after the sync only T is filled in
+            layout = _tile_layout(lib, big_guess, num_tiles, cam)
         StageTimer.mark("~sync")
         ready.synchronize()  # the one host sync
         M, T, zmin, zmax = (int(v) & 0xFFFFFFFF if i >= 2 else int(v) for i, v in enumerate(host.tolist()))
-        _T_SEEN[dev] = T
-        _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
         if not window_holds(window, zmin, zmax):
             # a visible depth outside the window: the sort's keys were clipped
+            _T_SEEN[dev] = T
+            _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
             return forward_pipeline(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit,
                                     sh_rest, sh_degree, pair_counts, depth_window_ok=False)
     else:
@@ -280,6 +306,9 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     fr.M, fr.T = M, T
 
     if M == 0:
+        if n > 0:
+            _T_SEEN[dev] = T
+            _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
         # renderer.py:74-83: bg once (not doubled, not clamped), zero alpha/depth
         bg = torch.tensor(cam.bg, dtype=f32, device=dev).view(3, 1, 1)
         image = bg.repeat(1, H, W)
@@ -288,46 +317,40 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         fr.pair_offset = torch.zeros((max(n, 1),), dtype=i32, device=dev)
         return image, alpha, depth, means2d, conics, radii, vis, fr
 
-    # The T-sized buffers live in one allocation addressed by pointer
-    # arithmetic: between the host sync and the blend launch the GPU idles,
-    # so this span does no torch work (views of the sorted ids and the bitmap
-    # are made after the blend is queued).
+    # Between the host sync and the blend launch the GPU idles: this span
+    # only fills T into the prepared launches (re-emitting first when T
+    # exceeded the guess); views of the buffers are made after the blend is
+    # queued.
     emitted = big_guess is not None and big_guess[1] >= T
-    big, cap_t = big_guess if emitted else _alloc_tile_buffers(lib, T, num_tiles, cam.cells, dev)
-    tws_bytes = int(lib.gs_radix_sort_workspace_bytes(T))
-    live_words = int(lib.gs_blend_live_words(T, num_tiles))
-    base = big.data_ptr()
-    p_tk = (base, base + 4 * cap_t)                   # tile keys, ping-pong
-    p_tv = (base + 8 * cap_t, base + 12 * cap_t)      # Gaussian ids, ping-pong
-    o_ws = (16 * cap_t + 255) // 256 * 256
-    o_live = o_ws + (int(lib.gs_radix_sort_workspace_bytes(cap_t)) + 255) // 256 * 256
-    p_ws, p_live = base + o_ws, base + o_live
     if not emitted:
-        ba.tile_keys, ba.pair_gauss, ba.capacity = p_tk[0], p_tv[0], cap_t
+        layout = _tile_layout(lib, _alloc_tile_buffers(lib, T, num_tiles, cam.cells, dev), num_tiles, cam)
+        ba.tile_keys, ba.pair_gauss, ba.capacity = layout.p_tk[0], layout.p_tv[0], layout.cap
         StageTimer.mark("bin_emit")
         N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
-
-    bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
+    L = layout
     alt = C.c_int32(0)
     StageTimer.mark("tile_sort")
-    N.check(lib.gs_radix_sort_pairs(p_tk[0], p_tv[0], p_tk[1], p_tv[1], T, 0, bits, 0,
-                                    p_ws, tws_bytes, C.byref(alt), s), "tile sort")
-    ra = N.GsRangeArgs(T, num_tiles, p_tk[alt.value], N.ptr(ranges))
+    N.check(lib.gs_radix_sort_pairs(L.p_tk[0], L.p_tv[0], L.p_tk[1], L.p_tv[1], T, 0, L.bits, 0,
+                                    L.p_ws, L.ws_bytes, C.byref(alt), s), "tile sort")
+    ra = N.GsRangeArgs(T, num_tiles, L.p_tk[alt.value], N.ptr(ranges))
     StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
-    fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), p_tv[alt.value], N.ptr(records),
+    fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), L.p_tv[alt.value], N.ptr(records),
                           N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state),
-                          p_live, live_words, N.ptr(pair_counts))
+                          L.p_live, L.live_words, N.ptr(pair_counts))
     StageTimer.mark("blend_fwd")
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
     StageTimer.mark("~end_fwd")
+    _T_SEEN[dev] = T  # (the next frame's guesses: after the launches)
+    _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
 
     # (the blend is queued: views for the frame cost no GPU idle time now)
-    kv = big[:16 * cap_t].view(i32).view(4, cap_t)
+    kv = L.big[:16 * L.cap].view(i32).view(4, L.cap)
     fr.sorted_gauss = kv[2 + alt.value, :T]
-    fr.live_bits = big[o_live:o_live + 8 * cam.cells * live_words].view(torch.int64).view(cam.cells, live_words)
-    fr.big = big
+    fr.live_bits = L.big[L.o_live:L.o_live + 8 * cam.cells * L.live_words].view(torch.int64).view(cam.cells,
+                                                                                               L.live_words)
+    fr.big = L.big
     fr.pair_offset, fr.ranges = pair_offset, ranges
     fr.pix_acc, fr.pix_state = pix_acc, pix_state
     return image, alpha, depth, means2d, conics, radii, vis, fr
