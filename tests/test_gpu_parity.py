@@ -230,6 +230,26 @@ def test_radix_sort_matches_stable_argsort(pkg, cuda):
         assert np.array_equal(kk[alt.value].cpu().numpy().view(np.uint32), k[order]), (n, bits, lo, iota)
 
 
+def test_forward_capacity_paths(pkg, cuda):
+    """The forward queues the emission before the T read-back into buffers
+    sized from the last frame's T (+ 25 %); a frame whose T outgrows that
+    guess is emitted again after the read-back.  Both paths give the same
+    frame bit for bit."""
+    W, H = 320, 240
+    small = pkg.synthetic.make_scene(2000, W, H, seed=61)
+    big = pkg.synthetic.make_scene(20000, W, H, seed=62)
+    r = pkg.GaussianRenderer()
+    cam = Cam(W, H, small.fovx, small.fovy)
+    st = pkg.RenderSettings(H, W, torch.tensor([0.1, 0.2, 0.3]))
+    mb = pkg.synthetic.to_model(big, pkg.GaussianModel, cuda)
+    with torch.no_grad():
+        r.render(cam, pkg.synthetic.to_model(small, pkg.GaussianModel, cuda), st)
+        a = r.render(cam, mb, st)  # T far above the small frame's: the redo path
+        b = r.render(cam, mb, st)  # the same T again: emitted before the read-back
+    for key in ("image", "alpha", "depth"):
+        assert torch.equal(a[key], b[key]), key
+
+
 def test_tile_ranges_every_tile(pkg, cuda):
     """gs_tile_ranges writes every tile, empty ones as [p, p) (no memset), and
     all-empty lists."""
