@@ -499,12 +499,39 @@ def rasterize(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity,
     {name: tensor} buffers the gradient kernels write into (names xyz,
     scaling, rotation, color, opacity, sh_rest; see backward_pipeline)."""
     _check_inputs(xyz)
+    n = int(xyz.shape[0]) if xyz.dim() == 2 else -1
+    if n < 0 or xyz.shape[1] != 3:
+        raise ValueError(f"xyz must be [N, 3], got {tuple(xyz.shape)}")
+
+    def prep(name, t, tail):
+        """Same device as xyz, N rows of `tail` trailing shape, fp32 (other
+        float dtypes are cast, the cast on the autograd tape): the kernels read
+        raw fp32 rows, so anything else would be read as garbage."""
+        if t is None:
+            return None
+        if t.device != xyz.device:
+            raise RuntimeError(f"{name} is on {t.device}, the Gaussians' xyz on {xyz.device}")
+        if not t.is_floating_point():
+            raise TypeError(f"{name} must be a floating-point tensor, got {t.dtype}")
+        if t.dim() == 0 or t.shape[0] != n or t.numel() != n * math.prod(tail):
+            raise ValueError(f"{name} must hold {list(tail)} per Gaussian for N = {n}, got {tuple(t.shape)}")
+        return t if t.dtype == torch.float32 else t.float()
+
+    xyz = prep("xyz", xyz, (3,))
+    cov3d = prep("cov3d", cov3d, (3, 3))
+    scaling = prep("scaling", scaling, (3,))
+    rotation = prep("rotation", rotation, (4,))
+    logits = prep("colour", logits, (3,))
+    opacity = prep("opacity", opacity, (1,))
+    if cov3d is None and (scaling is None or rotation is None):
+        raise ValueError("need a covariance or scaling + rotation")
     sh_degree = int(sh_degree)
     if not 0 <= sh_degree <= 3:
         raise ValueError(f"sh_degree must be in 0..3, got {sh_degree}")
     if sh_degree > 0:
         if sh_rest is None or tuple(sh_rest.shape[1:]) != (N.GS_SH_REST, 3):
             raise ValueError("sh_degree > 0 needs sh_rest of shape [N, 15, 3]")
+        sh_rest = prep("sh_rest", sh_rest, (N.GS_SH_REST, 3))
         if sh_rest.stride(2) != 1 or sh_rest.stride(1) != 3:
             sh_rest = sh_rest.contiguous()
     else:

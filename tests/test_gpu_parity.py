@@ -574,3 +574,28 @@ def test_no_gaussians(pkg, cuda):
     assert out["viewspace_points"].shape == (0, 2) and out["radii"].shape == (0,)
     out["viewspace_points"].sum().backward()
     assert g.xyz.grad is not None and g.xyz.grad.shape == (0, 3)
+
+
+def test_float64_inputs_cast(pkg, cuda):
+    """Stub Gaussians in float64 (the reference's torch code would accept
+    them): rendered as their fp32 cast, gradients flowing back to the fp64
+    leaves; an input on another device raises instead of being read."""
+    cam = Cam(64, 64, np.radians(60), np.radians(60))
+    st = pkg.RenderSettings(64, 64, torch.zeros(3))
+    args = ([[0, 0, 1], [0.1, 0, 2]], np.stack([np.diag([1e-3] * 3)] * 2), [[1, 0, 0], [0, 1, 0]], [0.5, 0.7])
+    g32 = Gauss(*args, cuda)
+    g64 = Gauss(*args, cuda)
+    for name in ("xyz", "cov", "feats", "op"):
+        setattr(g64, name, getattr(g64, name).detach().double().requires_grad_())
+    a = pkg.GaussianRenderer().render(cam, g32, st)
+    b = pkg.GaussianRenderer().render(cam, g64, st)
+    for k in ("image", "alpha", "depth"):
+        assert torch.equal(a[k], b[k]), k
+    (a["image"].sum() + a["depth"].sum()).backward()
+    (b["image"].sum() + b["depth"].sum()).backward()
+    assert g64.xyz.grad.dtype == torch.float64
+    assert torch.allclose(g64.xyz.grad.float(), g32.xyz.grad) and torch.allclose(g64.op.grad.float(), g32.op.grad)
+    g_bad = Gauss(*args, cuda)
+    g_bad.op = g_bad.op.detach().cpu()
+    with pytest.raises(RuntimeError, match="opacity"):
+        pkg.GaussianRenderer().render(cam, g_bad, st)

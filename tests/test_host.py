@@ -125,3 +125,35 @@ def test_depth_window_choice(pkg):
     assert RZ.window_holds(None, bits(0.01), bits(1e30))
     base, nb = RZ.depth_window(bits(3.0), bits(3.0))  # a single depth
     assert nb >= 1 and RZ.window_holds((base, nb), bits(3.0), bits(3.0))
+
+
+def test_render_input_validation(pkg, monkeypatch):
+    """Inputs the kernels would misread raise before any launch: wrong row
+    counts or shapes, non-float dtypes, a missing covariance; other float
+    dtypes are cast to fp32 (on the autograd tape)."""
+    import sys
+    R = sys.modules[pkg.__name__ + ".rasterizer"]
+    monkeypatch.setattr(R, "_check_inputs", lambda x: None)  # (no HIP device here)
+    n = 4
+
+    def call(**kw):
+        a = dict(xyz=torch.zeros(n, 3), cov3d=torch.zeros(n, 3, 3), scaling=None, rotation=None,
+                 logits=torch.zeros(n, 3), opacity=torch.zeros(n))
+        a.update(kw)
+        R.rasterize(None, a["xyz"], a["cov3d"], a["scaling"], a["rotation"], a["logits"], a["opacity"])
+
+    with pytest.raises(ValueError, match="opacity"):
+        call(opacity=torch.zeros(n + 1))
+    with pytest.raises(ValueError, match="cov3d"):
+        call(cov3d=torch.zeros(n, 3))
+    with pytest.raises(ValueError, match="xyz"):
+        call(xyz=torch.zeros(n, 2))
+    with pytest.raises(TypeError, match="colour"):
+        call(logits=torch.zeros(n, 3, dtype=torch.int32))
+    with pytest.raises(ValueError, match="covariance"):
+        call(cov3d=None)
+    with pytest.raises(ValueError, match="rotation"):
+        call(cov3d=None, scaling=torch.zeros(n, 3), rotation=torch.zeros(n, 3))
+    # fp64 passes validation (cast), then reaches the launch path (camera None here)
+    with pytest.raises(AttributeError):
+        call(logits=torch.zeros(n, 3, dtype=torch.float64))
