@@ -119,11 +119,11 @@ def test_all_culled_returns_bg(pkg, cuda):
     assert g.xyz.grad is not None and torch.isfinite(g.xyz.grad).all()
 
 
-def _oracle_scene(sc, cov, bg):
+def _oracle_scene(sc, cov, bg, wv=None):
     o = G.oracle()
     return o.Scene(xyz=sc.xyz.numpy(), cov3d=cov, color_logits=sc.features_dc[:, 0].numpy(),
-                   opacity=torch.sigmoid(sc.opacity[:, 0]).numpy(), wv=np.eye(4), width=sc.width,
-                   height=sc.height, fovx=sc.fovx, fovy=sc.fovy, bg=np.asarray(bg, np.float32))
+                   opacity=torch.sigmoid(sc.opacity[:, 0]).numpy(), wv=np.eye(4) if wv is None else wv,
+                   width=sc.width, height=sc.height, fovx=sc.fovx, fovy=sc.fovy, bg=np.asarray(bg, np.float32))
 
 
 @pytest.mark.parametrize("n,w,h,sig", [(3000, 200, 152, (0.01, 0.05)), (20000, 320, 240, (0.002, 0.02))])
@@ -359,7 +359,7 @@ def test_long_tile_lists_vs_oracle(pkg, cuda, bg):
     assert not errs, errs
 
 
-def _scene_vs_oracle(pkg, cuda, sc, W, H, bg, seed=1, renderer_kw=None, knife=True, label=""):
+def _scene_vs_oracle(pkg, cuda, sc, W, H, bg, seed=1, renderer_kw=None, knife=True, label="", wv=None):
     """Render sc (this package's model, raw-parameter path) fwd + bwd of a
     seeded cotangent and compare with the oracle on the same inputs.  With
     knife=True, pixels out of tolerance are accepted only where the oracle's
@@ -368,13 +368,14 @@ def _scene_vs_oracle(pkg, cuda, sc, W, H, bg, seed=1, renderer_kw=None, knife=Tr
     import os
     m = pkg.synthetic.to_model(sc, pkg.GaussianModel, cuda)
     kw = renderer_kw or {}
-    out = pkg.GaussianRenderer(**kw).render(Cam(W, H, sc.fovx, sc.fovy), m, pkg.RenderSettings(H, W, torch.tensor(bg)))
+    out = pkg.GaussianRenderer(**kw).render(Cam(W, H, sc.fovx, sc.fovy, wv=wv), m,
+                                            pkg.RenderSettings(H, W, torch.tensor(bg)))
     rng = np.random.default_rng(seed)
     gi, ga, gd = (rng.uniform(-1, 1, s).astype(np.float32) for s in ((3, H, W), (1, H, W), (1, H, W)))
     L = sum((out[k] * torch.tensor(v, device=cuda)).sum() for k, v in (("image", gi), ("alpha", ga), ("depth", gd)))
     L.backward()
     cov = G.oracle().covariance(sc.scaling.numpy(), sc.rotation.numpy())
-    osc = _oracle_scene(sc, cov, bg)
+    osc = _oracle_scene(sc, cov, bg, wv=wv)
     osc.tile = kw.get("tile_size", 16)
     osc.radius_min, osc.radius_max = kw.get("radius_min", 0.01), kw.get("radius_max", 50.0)
     ref = G.oracle().render_backward(osc, gi, ga, gd, nthreads=min(16, os.cpu_count() or 1), margins=True)
@@ -421,6 +422,24 @@ def test_c2_full_size_vs_oracle(pkg, cuda):
     sc = pkg.synthetic.make_scene(100_000, W, H, seed=2)
     errs, bad, knife = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.2, 0.3, 0.4), seed=3, label="C2")
     assert bad.sum() <= 16, f"{int(bad.sum())} knife-edge pixels"
+    assert not errs, errs
+
+
+def test_c2_posed_camera_vs_oracle(pkg, cuda):
+    """C2 size through a rotated, translated camera (world_view_transform not
+    the identity: the projection's Rv, Tv and the y flip at scale), fwd + bwd
+    vs the oracle."""
+    W, H = 800, 800
+    sc = pkg.synthetic.make_scene(100_000, W, H, seed=12)
+    ax, ay = np.radians(6.0), np.radians(-9.0)
+    rx = np.array([[1, 0, 0], [0, np.cos(ax), -np.sin(ax)], [0, np.sin(ax), np.cos(ax)]])
+    ry = np.array([[np.cos(ay), 0, np.sin(ay)], [0, 1, 0], [-np.sin(ay), 0, np.cos(ay)]])
+    wv = np.eye(4)
+    wv[:3, :3] = ry @ rx
+    wv[:3, 3] = [0.12, -0.07, 0.25]
+    errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.05, 0.1, 0.0), seed=4, label="C2 posed",
+                                    wv=wv.astype(np.float32))
+    assert bad.sum() <= 16
     assert not errs, errs
 
 
