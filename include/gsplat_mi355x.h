@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 9
+#define GS_ABI_VERSION 10
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
@@ -196,6 +196,9 @@ typedef struct gs_range_args {
   int32_t num_tiles;
   const uint32_t *sorted_keys; /* [T] tile ids, sorted */
   uint32_t *ranges;            /* [num_tiles,2] */
+  uint8_t *slot_live;          /* optional (NULL: none): zeroed here, [T, cells] -- the backward's
+                                  gs_blend_bwd_args.slot_live, cleared without a kernel of its own */
+  int32_t cells;               /* gs_tile_quads(tile_size), with slot_live */
 } gs_range_args;
 gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream);
 

@@ -27,7 +27,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between cell partials in pair_grads (dense)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 9
+GS_ABI_VERSION = 10
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -72,6 +72,7 @@ class GsBinArgs(C.Structure):
 class GsRangeArgs(C.Structure):
     _fields_ = [
         ("num_pairs", C.c_int32), ("num_tiles", C.c_int32), ("sorted_keys", _vp), ("ranges", _vp),
+        ("slot_live", _vp), ("cells", C.c_int32),
     ]
 
 

@@ -824,6 +824,12 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
 __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
   const long long p = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (p > a.num_pairs) return;
+  if (a.slot_live && p < a.num_pairs) {  // slot p's flags for the backward (coalesced)
+    if (a.cells == 4)
+      reinterpret_cast<uint32_t *>(a.slot_live)[p] = 0u;
+    else
+      for (int c = 0; c < a.cells; ++c) a.slot_live[p * a.cells + c] = 0;
+  }
   const long long prev = p > 0 ? (long long)a.sorted_keys[p - 1] : -1;
   const long long cur = p < a.num_pairs ? (long long)a.sorted_keys[p] : (long long)a.num_tiles;
   if (cur == prev) return;
@@ -1927,6 +1933,8 @@ gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream) {
   if (a->num_pairs < 0 || a->num_tiles < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative size", "gs_tile_ranges");
   if (a->num_tiles == 0) return GS_OK;
   if (a->num_pairs > 0 && !a->sorted_keys) return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_ranges");
+  if (a->slot_live && (a->cells < 1 || (a->cells == 4 && (reinterpret_cast<uintptr_t>(a->slot_live) & 3u))))
+    return fail(GS_ERR_INVALID_ARG, "%s: slot_live needs cells >= 1 (4-B aligned at 4 cells)", "gs_tile_ranges");
   k_tile_ranges<<<div_up(a->num_pairs + 1, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_tile_ranges");
 }

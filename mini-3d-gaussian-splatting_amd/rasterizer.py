@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -145,11 +146,12 @@ def _check_inputs(xyz: torch.Tensor):
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
     __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_acc",
-                 "pix_state", "live_bits", "big", "M", "T")
+                 "pix_state", "live_bits", "big", "M", "T", "slot_live")
 
 
 _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess)
 _HOST_COUNTERS: dict = {}  # device -> pinned int32[4] for the (M, T, depth-bits range) read-back
+_FUSE_FLAGS = os.environ.get("GS_FUSE_SLOT_FLAGS", "1") != "0"  # slot flags zeroed by gs_tile_ranges
 _DEPTH_WINDOW: dict = {}  # device -> (key_base, key_bits) from its last frame's visible depth range
 
 
@@ -176,11 +178,12 @@ def window_holds(window, zmin_bits: int, zmax_bits: int) -> bool:
 
 def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cells: int, dev):
     """One byte buffer for T <= cap entries: tile keys + Gaussian ids
-    (ping-pong, 16 B/entry), the tile sort's workspace and the liveness
-    bitmap (cells x gs_blend_live_words)."""
+    (ping-pong, 16 B/entry), the tile sort's workspace, the liveness bitmap
+    (cells x gs_blend_live_words) and the backward's slot flags (cells B/entry)."""
     nbytes = (16 * cap + 255) // 256 * 256
     nbytes += (int(lib.gs_radix_sort_workspace_bytes(cap)) + 255) // 256 * 256
     nbytes += 8 * cells * int(lib.gs_blend_live_words(cap, num_tiles))
+    nbytes += (cells * cap + 255) // 256 * 256  # the backward's slot flags (zeroed by gs_tile_ranges)
     return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
 
 
@@ -188,7 +191,8 @@ class _TileLayout:
     """Addresses inside one _alloc_tile_buffers allocation of capacity `cap`:
     tile keys and Gaussian ids (ping-pong), the tile sort's workspace, the
     liveness bitmap (stride live_words, sized for `cap` entries)."""
-    __slots__ = ("big", "cap", "p_tk", "p_tv", "p_ws", "ws_bytes", "o_live", "p_live", "live_words", "bits")
+    __slots__ = ("big", "cap", "p_tk", "p_tv", "p_ws", "ws_bytes", "o_live", "p_live", "live_words", "bits",
+                 "o_flags")
 
 
 def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
@@ -203,12 +207,13 @@ def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
     L.o_live = o_ws + (L.ws_bytes + 255) // 256 * 256
     L.p_ws, L.p_live = base + o_ws, base + L.o_live
     L.live_words = int(lib.gs_blend_live_words(cap, num_tiles))
+    L.o_flags = L.o_live + 8 * cam.cells * L.live_words
     L.bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
     return L
 
 
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
-                     sh_rest=None, sh_degree=0, pair_counts=None, depth_window_ok=True):
+                     sh_rest=None, sh_degree=0, pair_counts=None, depth_window_ok=True, need_grad=False):
     """pair_counts: optional int32 [H*W] the blend fills with each pixel's
     contributing pairs (a measurement counter; not in render()).
 
@@ -245,6 +250,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     N.check(lib.gs_project_forward(C.byref(pa), s), "gs_project_forward")
 
     fr = _Frame()
+    fr.slot_live = None
     fr.records, fr.rects, fr.vis, fr.order = records, rects, vis, None
     if n > 0:
         ws = torch.empty((lib.gs_radix_sort_workspace_bytes(n),), dtype=torch.uint8, device=dev)
@@ -300,7 +306,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
             _T_SEEN[dev] = T
             _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
             return forward_pipeline(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit,
-                                    sh_rest, sh_degree, pair_counts, depth_window_ok=False)
+                                    sh_rest, sh_degree, pair_counts, depth_window_ok=False, need_grad=need_grad)
     else:
         M, T = 0, 0
     fr.M, fr.T = M, T
@@ -332,7 +338,9 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     StageTimer.mark("tile_sort")
     N.check(lib.gs_radix_sort_pairs(L.p_tk[0], L.p_tv[0], L.p_tk[1], L.p_tv[1], T, 0, L.bits, 0,
                                     L.p_ws, L.ws_bytes, C.byref(alt), s), "tile sort")
-    ra = N.GsRangeArgs(T, num_tiles, L.p_tk[alt.value], N.ptr(ranges))
+    # (with gradients to come: the backward's slot flags zeroed in the same kernel)
+    ra = N.GsRangeArgs(T, num_tiles, L.p_tk[alt.value], N.ptr(ranges),
+                       L.big.data_ptr() + L.o_flags if need_grad else None, cam.cells)
     StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
@@ -351,6 +359,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     fr.live_bits = L.big[L.o_live:L.o_live + 8 * cam.cells * L.live_words].view(torch.int64).view(cam.cells,
                                                                                                L.live_words)
     fr.big = L.big
+    fr.slot_live = L.big[L.o_flags:L.o_flags + cam.cells * T] if need_grad else None
     fr.pair_offset, fr.ranges = pair_offset, ranges
     fr.pix_acc, fr.pix_state = pix_acc, pix_state
     return image, alpha, depth, means2d, conics, radii, vis, fr
@@ -382,7 +391,9 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         # one partial per (slot, 8x8 cell of the tile); only the cells that
         # replay an entry write theirs and set its flag
         pair_grads = torch.empty((fr.T * cam.cells, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
-        slot_live = torch.zeros((fr.T * cam.cells,), dtype=torch.uint8, device=dev)
+        slot_live = fr.slot_live  # (zeroed by the forward's gs_tile_ranges)
+        if slot_live is None:
+            slot_live = torch.zeros((fr.T * cam.cells,), dtype=torch.uint8, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
@@ -460,7 +471,8 @@ class RasterizeGaussians(torch.autograd.Function):
     def forward(ctx, xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, cam: CameraParams,
                 opacity_is_logit=False, sh_degree=0, grad_dest=None):
         image, alpha, depth, means2d, conics, radii, vis, fr = forward_pipeline(
-            cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
+            cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree,
+            need_grad=_FUSE_FLAGS and any(ctx.needs_input_grad[:7]))
         ctx.cam, ctx.frame, ctx.opacity_is_logit, ctx.sh_degree = cam, fr, opacity_is_logit, sh_degree
         ctx.grad_dest = grad_dest
         ctx.save_for_backward(xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics)
