@@ -546,6 +546,48 @@ def test_grad_bucket_adoption(pkg, cuda):
         assert torch.equal(a, b)
 
 
+def test_rccl_range_reduction_world1(pkg, cuda):
+    """The RCCL path itself (backend nccl, world size 1, in this process): the
+    backward hands its rows over in ranges, each range's five parameter
+    slices reduced as one coalesced collective; the gradients equal a plain
+    backward's bit for bit (a mean over one rank)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    if dist.is_initialized():
+        pytest.skip("a process group already exists")
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(cuda))
+    try:
+        syn = pkg.synthetic
+        sc = syn.make_scene(20000, 320, 240, seed=5)
+        res = []
+        for ranges in (0, 1, 3):
+            m = syn.to_model(sc, pkg.GaussianModel, cuda)
+            params = m.grad_parameters()
+            red = None
+            if ranges:
+                red = pkg.distributed.GradAllReduce(params, chunks=ranges, min_chunk_rows=4096).attach(m)
+                assert red._coalesce
+            out = pkg.GaussianRenderer().render(Cam(320, 240, sc.fovx, sc.fovy), m,
+                                                pkg.RenderSettings(240, 320, torch.zeros(3)))
+            (out["image"].sum() + out["alpha"].sum() + out["depth"].sum()).backward()
+            if red is not None:
+                assert red.ranges_reduced == ranges
+                red.all_reduce_mean()
+            torch.cuda.synchronize()
+            res.append([p.grad.clone() for p in params])
+        for other in res[1:]:
+            for a, b in zip(res[0], other):
+                assert torch.equal(a, b)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_depth_window_miss_rerenders(pkg, cuda):
     """The depth sort runs over a window of key bits chosen from the previous
     frame's visible depth range (rasterizer.depth_window); a frame whose depths
