@@ -19,6 +19,7 @@ from __future__ import annotations
 import ctypes as C
 import math
 import os
+import threading
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -150,7 +151,10 @@ class _Frame:
 
 
 _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess)
-_HOST_COUNTERS: dict = {}  # device -> pinned int32[4] for the (M, T, depth-bits range) read-back
+# per host thread: device -> pinned int32[4] for the (M, T, depth-bits range)
+# read-back (renders from several threads each read their own counters; the
+# two per-device guesses above are only guesses, a stale one is corrected)
+_HOST_COUNTERS = threading.local()
 _FUSE_FLAGS = os.environ.get("GS_FUSE_SLOT_FLAGS", "1") != "0"  # slot flags zeroed by gs_tile_ranges
 _DEPTH_WINDOW: dict = {}  # device -> (key_base, key_bits) from its last frame's visible depth range
 
@@ -284,9 +288,12 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, cam.cells, dev) if cap else None
         # (M, T) read back through pinned memory, copied BEFORE the emission
         # is queued, so the host wakes while the GPU still emits
-        host = _HOST_COUNTERS.get(dev)
+        per_thread = getattr(_HOST_COUNTERS, "bufs", None)
+        if per_thread is None:
+            per_thread = _HOST_COUNTERS.bufs = {}
+        host = per_thread.get(dev)
         if host is None:
-            host = _HOST_COUNTERS[dev] = torch.empty((4,), dtype=i32, pin_memory=True)
+            host = per_thread[dev] = torch.empty((4,), dtype=i32, pin_memory=True)
         host.copy_(counters[:4], non_blocking=True)
         ready = torch.cuda.Event()
         ready.record()

@@ -660,3 +660,44 @@ def test_float64_inputs_cast(pkg, cuda):
     g_bad.op = g_bad.op.detach().cpu()
     with pytest.raises(RuntimeError, match="opacity"):
         pkg.GaussianRenderer().render(cam, g_bad, st)
+
+
+def test_concurrent_renders_two_threads(pkg, cuda):
+    """SURVEY 8(b) threading row: renders from two host threads on their own
+    streams, concurrently, give each thread's frames exactly as a lone render
+    does (each thread reads back its own counters)."""
+    import threading
+    syn = pkg.synthetic
+    W, H = 320, 240
+    scenes = [syn.make_scene(n, W, H, seed=70 + i) for i, n in enumerate((15000, 40000))]
+    models = [syn.to_model(sc, pkg.GaussianModel, cuda) for sc in scenes]
+    st = pkg.RenderSettings(H, W, torch.tensor([0.1, 0.1, 0.1]))
+
+    def render(i):
+        with torch.no_grad():
+            return pkg.GaussianRenderer().render(Cam(W, H, scenes[i].fovx, scenes[i].fovy), models[i], st)["image"]
+    want = [render(0).clone(), render(1).clone()]
+    torch.cuda.synchronize()
+    got = [[], []]
+    errors = []
+
+    def worker(i):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for _ in range(6):
+                    got[i].append(render(i).clone())
+            s.synchronize()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+    for i in (0, 1):
+        assert len(got[i]) == 6
+        for img in got[i]:
+            assert torch.equal(img, want[i]), i
