@@ -45,6 +45,7 @@ static void run(int n, int bits, int iota) {
 
 int main() {
   run(1000000, 32, 1);
+  run(1000000, 24, 1);  // the depth sort over its key window (C3: 24 bits)
   run(4400000, 13, 0);
   return 0;
 }
