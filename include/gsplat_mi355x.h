@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 10
+#define GS_ABI_VERSION 11
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
@@ -152,6 +152,22 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
                               int32_t end_bit, int32_t vals_are_iota, void *workspace,
                               size_t workspace_bytes, int32_t *result_in_alt,
                               gs_stream_t stream);
+
+/* Windowed depth keys (9 <= key_bits <= 24, gs_project_args.key_bits): the
+ * same result as gs_radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, 0,
+ * key_bits, 1, ...) -- values = input positions, stable -- in one 8-bit MSD
+ * pass plus one LDS-resident sort per top-digit bucket (one workgroup each).
+ * The result is always in (keys_alt, vals_alt) (*result_in_alt = 1).
+ * Preconditions: visible keys < 255 << (key_bits - 8); 2^key_bits - 1 is the
+ * culled sentinel (its bucket stays in index order).  A bucket of more than
+ * 16384 keys is left unsorted and 0xFFFFFFFF is stored to *overflow_word
+ * (renderer: the depth-max word of gs_project_args.key_minmax, so the frame's
+ * window check fails and it is sorted again with gs_radix_sort_pairs).
+ * Workspace: gs_radix_sort_workspace_bytes(n).  key_bits outside 9..24
+ * returns GS_ERR_UNSUPPORTED. */
+gs_status gs_depth_sort_msd(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
+                            int32_t n, int32_t key_bits, void *workspace, size_t workspace_bytes,
+                            uint32_t *overflow_word, int32_t *result_in_alt, gs_stream_t stream);
 
 /* ---- Stage 3: tile binning (renderer.py:263-298) ----------------------
  * gs_bin_count: per-Gaussian tile-touch counts and visibility in depth order,

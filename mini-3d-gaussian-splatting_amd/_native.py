@@ -27,7 +27,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between cell partials in pair_grads (dense)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 10
+GS_ABI_VERSION = 11
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -155,7 +155,7 @@ class GsDensifyArgs(C.Structure):
 # Every symbol the header declares (checked by tests/test_abi.py).
 EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
-    "gs_radix_sort_pairs", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
+    "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
     "gs_tile_ranges", "gs_blend_live_words", "gs_tile_quads", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
     "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
     "gs_densify_workspace_bytes", "gs_densify_count", "gs_densify_emit",
@@ -178,6 +178,8 @@ def _declare(lib):
     lib.gs_radix_sort_workspace_bytes.restype = C.c_size_t
     lib.gs_radix_sort_pairs.argtypes = [_vp, _vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                         _vp, C.c_size_t, P(C.c_int32), _vp]
+    lib.gs_depth_sort_msd.argtypes = [_vp, _vp, _vp, _vp, C.c_int32, C.c_int32, _vp, C.c_size_t, _vp,
+                                      P(C.c_int32), _vp]
     lib.gs_bin_workspace_bytes.argtypes = [C.c_int32]
     lib.gs_bin_workspace_bytes.restype = C.c_size_t
     lib.gs_bin_count.argtypes = [P(GsBinArgs), _vp]
@@ -199,7 +201,7 @@ def _declare(lib):
     lib.gs_densify_workspace_bytes.restype = C.c_size_t
     lib.gs_densify_count.argtypes = [P(GsDensifyArgs), _vp]
     lib.gs_densify_emit.argtypes = [P(GsDensifyArgs), _vp]
-    for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_bin_count", "gs_bin_emit",
+    for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_count", "gs_bin_emit",
               "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
               "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
         getattr(lib, f).restype = C.c_int

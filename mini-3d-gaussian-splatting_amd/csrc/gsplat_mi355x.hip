@@ -578,6 +578,141 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
   }
 }
 
+// Bucket sort after one MSD pass (gs_depth_sort_msd): workgroup d sorts the
+// items whose top 8 key bits are d -- a contiguous, index-ordered run of the
+// MSD pass's output -- by their low `lowbits` bits, in LDS, in place.  Stable
+// LSD passes as in k_radix_scatter (wave w owns a contiguous segment, walked
+// in rounds of 64; ballot match ranking), but the data stays in LDS between
+// passes.  Bucket 255 holds the culled sentinel only (the caller's window
+// keeps visible keys below 255 << lowbits) and is left as the MSD pass wrote
+// it: index order, what the LSD sort gives equal keys.  A bucket over
+// kMsdCap items is left unsorted and flagged: 0xFFFFFFFF in *overflow (the
+// caller's depth-max word, so its window check fails and it sorts again).
+constexpr int kMsdThreads = 1024;
+constexpr int kMsdWaves = kMsdThreads / kWave;
+constexpr int kMsdIpt = 16;
+constexpr int kMsdCap = kMsdThreads * kMsdIpt;  // 16384 items: 128 KB of keys + values in LDS
+
+__global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__restrict__ keys,
+                                                               uint32_t *__restrict__ vals,
+                                                               const uint32_t *__restrict__ totals, int lowbits,
+                                                               uint32_t *overflow) {
+  __shared__ uint32_t s_k[kMsdCap], s_v[kMsdCap];
+  __shared__ uint32_t wcnt[kMsdWaves][kRadix];
+  __shared__ uint32_t s_lbase[kRadix];
+  __shared__ uint32_t s_tmp[4];
+  __shared__ uint32_t s_seg[2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t d0 = blockIdx.x;  // the bucket (grid: 255; bucket 255 is never sorted)
+  if (wave == 0) {
+    // start = totals[0 .. d0) summed, size = totals[d0]
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t t = (uint32_t)(4 * lane + k);
+      s += t < d0 ? totals[t] : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o, 64);
+    if (lane == 0) {
+      s_seg[0] = s;
+      s_seg[1] = totals[d0];
+    }
+  }
+  __syncthreads();
+  const uint32_t start = s_seg[0], size = s_seg[1];
+  if (size <= 1u) return;
+  if (size > (uint32_t)kMsdCap) {
+    if (threadIdx.x == 0) *overflow = 0xFFFFFFFFu;
+    return;
+  }
+  // wave w: items [w seg, (w + 1) seg), seg a multiple of 64; order (wave, round, lane)
+  const uint32_t seg = (size + kMsdThreads - 1) / kMsdThreads * kWave;
+  const int rounds = (int)(seg / kWave);
+  uint32_t k_[kMsdIpt], v_[kMsdIpt];
+#pragma unroll
+  for (int r = 0; r < kMsdIpt; ++r) {
+    const uint32_t i = (uint32_t)wave * seg + (uint32_t)(r * kWave + lane);
+    const bool ok = r < rounds && i < size;
+    k_[r] = ok ? keys[start + i] : 0u;
+    v_[r] = ok ? vals[start + i] : 0u;
+  }
+  const int passes = (lowbits + kRadixBits - 1) / kRadixBits;
+  int shift = 0;
+  for (int p = 0; p < passes; ++p) {
+    const int nbits = (lowbits - shift + (passes - p) - 1) / (passes - p);
+    const uint32_t mask = (1u << nbits) - 1u;
+    for (int t = threadIdx.x; t < kMsdWaves * kRadix; t += kMsdThreads) (&wcnt[0][0])[t] = 0u;
+    __syncthreads();
+    uint32_t rk[kMsdIpt];
+#pragma unroll
+    for (int r = 0; r < kMsdIpt; ++r) {
+      rk[r] = 0xFFFFFFFFu;
+      if (r < rounds) {  // wave-uniform
+        const uint32_t i = (uint32_t)wave * seg + (uint32_t)(r * kWave + lane);
+        const bool valid = i < size;
+        const uint32_t dg = (k_[r] >> shift) & mask;
+        const unsigned long long m = match_digit(dg, nbits, __ballot(valid));
+        const uint32_t below = (uint32_t)__popcll(m & lanemask_lt());
+        uint32_t old = 0;
+        if (valid) old = wcnt[wave][dg];
+        if (valid && below == 0) wcnt[wave][dg] = old + (uint32_t)__popcll(m);
+        if (valid) rk[r] = old + below;
+      }
+    }
+    __syncthreads();
+    // per digit: wave prefixes, then the block-local digit start (scan over
+    // the 256 digits by the first four waves)
+    uint32_t run = 0;
+    if (threadIdx.x < kRadix) {
+      for (int w = 0; w < kMsdWaves; ++w) {
+        const uint32_t t = wcnt[w][threadIdx.x];
+        wcnt[w][threadIdx.x] = run;
+        run += t;
+      }
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (threadIdx.x < kRadix && lane == 63) s_tmp[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x < kRadix) {
+      uint32_t base = 0;
+      for (int w = 0; w < wave; ++w) base += s_tmp[w];
+      s_lbase[threadIdx.x] = base + incl - run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kMsdIpt; ++r) {
+      if (rk[r] != 0xFFFFFFFFu) {
+        const uint32_t dg = (k_[r] >> shift) & mask;
+        const uint32_t lp = s_lbase[dg] + wcnt[wave][dg] + rk[r];
+        s_k[lp] = k_[r];
+        s_v[lp] = v_[r];
+      }
+    }
+    __syncthreads();
+    shift += nbits;
+    if (p + 1 < passes) {
+#pragma unroll
+      for (int r = 0; r < kMsdIpt; ++r) {
+        const uint32_t i = (uint32_t)wave * seg + (uint32_t)(r * kWave + lane);
+        if (r < rounds && i < size) {
+          k_[r] = s_k[i];
+          v_[r] = s_v[i];
+        }
+      }
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < size; i += kMsdThreads) {
+    keys[start + i] = s_k[i];
+    vals[start + i] = s_v[i];
+  }
+}
+
 // ======================================================== binning =========
 // The binning workspace: 5 nb words of per-block partials, then the
 // depth-ordered rectangles (n uint2, 16-B aligned).
@@ -1891,6 +2026,30 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
     vout = tv;
   }
   return GS_OK;
+}
+
+gs_status gs_depth_sort_msd(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt, int32_t n,
+                            int32_t key_bits, void *workspace, size_t workspace_bytes, uint32_t *overflow_word,
+                            int32_t *result_in_alt, gs_stream_t stream) {
+  if (!result_in_alt) return fail(GS_ERR_INVALID_ARG, "%s: null result_in_alt", "gs_depth_sort_msd");
+  if (key_bits < 9 || key_bits > 24 || n < 0)
+    return fail(GS_ERR_UNSUPPORTED, "%s: key_bits must be 9..24", "gs_depth_sort_msd");
+  *result_in_alt = 1;
+  if (n == 0) return GS_OK;
+  if (!keys || !vals || !keys_alt || !vals_alt || !workspace || !overflow_word ||
+      workspace_bytes < gs_radix_sort_workspace_bytes(n))
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer or workspace too small", "gs_depth_sort_msd");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)div_up(n, kSortChunk);
+  uint32_t *counts = (uint32_t *)workspace;
+  uint32_t *totals = counts + (size_t)kRadix * nb;
+  const int shift = key_bits - kRadixBits;
+  k_radix_hist<<<nb, kBlock, 0, s>>>(keys, n, shift, kRadixBits, counts, nb);
+  k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, totals, nb);
+  k_radix_scatter<true><<<nb, kBlock, 0, s>>>(keys, nullptr, keys_alt, vals_alt, n, shift, kRadixBits, counts,
+                                               totals, nb);
+  k_msd_bucket_sort<<<kRadix - 1, kMsdThreads, 0, s>>>(keys_alt, vals_alt, totals, shift, overflow_word);
+  return check_launch("gs_depth_sort_msd");
 }
 
 size_t gs_bin_workspace_bytes(int32_t n) {

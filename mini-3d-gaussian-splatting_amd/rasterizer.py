@@ -157,6 +157,14 @@ _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess
 _HOST_COUNTERS = threading.local()
 _FUSE_FLAGS = os.environ.get("GS_FUSE_SLOT_FLAGS", "1") != "0"  # slot flags zeroed by gs_tile_ranges
 _DEPTH_WINDOW: dict = {}  # device -> (key_base, key_bits) from its last frame's visible depth range
+# Windowed depth keys of 9..24 bits are sorted by gs_depth_sort_msd (one MSD pass + a sort per
+# bucket in LDS) unless GS_DEPTH_MSD=0.  A bucket over its LDS capacity (clumped depths) poisons
+# the frame's depth max (0xFFFFFFFF): the frame is sorted again with the LSD passes, and the LSD
+# path is kept for the next _MSD_BACKOFF_FRAMES frames on that device.
+_DEPTH_MSD = os.environ.get("GS_DEPTH_MSD", "1") != "0"
+_MSD_BACKOFF: dict = {}  # device -> frames left on the LSD path after an overflow
+_MSD_BACKOFF_FRAMES = 64
+_POISON = 0xFFFFFFFF
 
 
 def depth_window(zmin_bits: int, zmax_bits: int):
@@ -169,7 +177,16 @@ def depth_window(zmin_bits: int, zmax_bits: int):
     lo = max(0, zmin_bits - span // 8 - 1)
     hi = zmax_bits + span // 8 + 1
     bits = max(1, (hi - lo + 1).bit_length())  # keys 0 .. hi - lo < 2^bits - 1 (the culled sentinel)
+    if bits >= 9 and hi - lo >= _msd_limit(bits):
+        bits += 1  # the MSD depth sort's top bucket is the sentinel's alone
     return (lo, bits) if (bits + 7) // 8 < 4 else None
+
+
+def _msd_limit(bits: int) -> int:
+    """Visible keys of a `bits`-bit window stay below this: 2^bits - 1 (the
+    culled sentinel) and, from 9 bits on, 255 << (bits - 8), so that the top
+    digit of gs_depth_sort_msd's MSD pass holds the sentinel only."""
+    return min((1 << bits) - 1, 255 << (bits - 8)) if bits >= 9 else (1 << bits) - 1
 
 
 def window_holds(window, zmin_bits: int, zmax_bits: int) -> bool:
@@ -177,7 +194,7 @@ def window_holds(window, zmin_bits: int, zmax_bits: int) -> bool:
     if window is None or zmin_bits > zmax_bits:
         return True
     base, bits = window
-    return zmin_bits >= base and zmax_bits - base < (1 << bits) - 1
+    return zmin_bits >= base and zmax_bits - base < _msd_limit(bits)
 
 
 def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cells: int, dev):
@@ -260,8 +277,16 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         ws = torch.empty((lib.gs_radix_sort_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         StageTimer.mark("depth_sort")
         alt = C.c_int32(0)
-        N.check(lib.gs_radix_sort_pairs(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n, 0,
-                                        key_bits, 1, N.ptr(ws), ws.numel(), C.byref(alt), s), "depth sort")
+        backoff = _MSD_BACKOFF.get(dev, 0)
+        if backoff:
+            _MSD_BACKOFF[dev] = backoff - 1
+        if _DEPTH_MSD and window is not None and 9 <= key_bits <= 24 and not backoff:
+            N.check(lib.gs_depth_sort_msd(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n,
+                                          key_bits, N.ptr(ws), ws.numel(), N.ptr(key_minmax) + 4, C.byref(alt),
+                                          s), "depth sort (msd)")
+        else:
+            N.check(lib.gs_radix_sort_pairs(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n, 0,
+                                            key_bits, 1, N.ptr(ws), ws.numel(), C.byref(alt), s), "depth sort")
         sorted_ids = vals[alt.value]
         fr.order = sorted_ids
         bws = torch.empty((lib.gs_bin_workspace_bytes(n),), dtype=torch.uint8, device=dev)
@@ -309,7 +334,10 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         ready.synchronize()  # the one host sync
         M, T, zmin, zmax = (int(v) & 0xFFFFFFFF if i >= 2 else int(v) for i, v in enumerate(host.tolist()))
         if not window_holds(window, zmin, zmax):
-            # a visible depth outside the window: the sort's keys were clipped
+            # a visible depth outside the window (the sort's keys were clipped),
+            # or an MSD bucket over capacity (the depth max poisoned)
+            if zmax == _POISON:
+                _MSD_BACKOFF[dev] = _MSD_BACKOFF_FRAMES
             _T_SEEN[dev] = T
             _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
             return forward_pipeline(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit,

@@ -230,6 +230,81 @@ def test_radix_sort_matches_stable_argsort(pkg, cuda):
         assert np.array_equal(kk[alt.value].cpu().numpy().view(np.uint32), k[order]), (n, bits, lo, iota)
 
 
+def test_depth_sort_msd_matches_stable_argsort(pkg, cuda):
+    """gs_depth_sort_msd (one MSD pass + a sort per bucket in LDS) gives the
+    LSD sort's result -- np.argsort(kind="stable") of the keys, values = input
+    positions -- for windowed keys below 255 << (bits - 8) plus culled
+    sentinels (2^bits - 1); a bucket over 16384 keys sets the overflow word."""
+    import ctypes as C
+    N = pkg._native
+    lib = N.load()
+    rng = np.random.default_rng(11)
+    # (n, bits, culled fraction, clumped): clumped = every visible key in two buckets
+    for n, bits, culled, clump in ((1, 9, 0.0, False), (5, 12, 0.4, False), (1000, 9, 0.1, False),
+                                   (100_000, 16, 0.0, False), (1_000_000, 24, 0.0, False),
+                                   (300_000, 20, 0.5, False), (40_000, 24, 0.0, True), (2049, 17, 1.0, False)):
+        lim = 255 << (bits - 8)
+        if clump:
+            k = (rng.integers(0, 2, n) << (bits - 8)) + rng.integers(0, 50, n)  # ~20k keys per bucket
+        else:
+            k = rng.integers(0, lim, n)
+        k = k.astype(np.uint32)
+        k[rng.random(n) < culled] = (1 << bits) - 1
+        kk = torch.empty((2, n), dtype=torch.int32, device=cuda)
+        vv = torch.full((2, n), -7, dtype=torch.int32, device=cuda)
+        kk[0].copy_(torch.tensor(k.view(np.int32)))
+        ws = torch.full((lib.gs_radix_sort_workspace_bytes(n),), 0xAB, dtype=torch.uint8, device=cuda)
+        flag = torch.zeros((2,), dtype=torch.int32, device=cuda)
+        alt = C.c_int32(0)
+        N.check(lib.gs_depth_sort_msd(N.ptr(kk[0]), N.ptr(vv[0]), N.ptr(kk[1]), N.ptr(vv[1]), n, bits, N.ptr(ws),
+                                      ws.numel(), N.ptr(flag) + 4, C.byref(alt), torch.cuda.current_stream().cuda_stream),
+                "msd sort")
+        torch.cuda.synchronize()
+        assert alt.value == 1
+        if clump:
+            assert int(flag[1]) == -1, "a bucket over capacity must set the overflow word"
+            continue
+        assert int(flag[1]) == 0, (n, bits)
+        order = np.argsort(k, kind="stable")
+        assert np.array_equal(vv[1].cpu().numpy().view(np.uint32), order.astype(np.uint32)), (n, bits)
+        assert np.array_equal(kk[1].cpu().numpy().view(np.uint32), k[order]), (n, bits)
+    with pytest.raises(RuntimeError):
+        N.check(lib.gs_depth_sort_msd(N.ptr(kk[0]), N.ptr(vv[0]), N.ptr(kk[1]), N.ptr(vv[1]), 10, 32, N.ptr(ws),
+                                      ws.numel(), N.ptr(flag), C.byref(alt), None), "msd sort")
+
+
+def test_depth_sort_msd_overflow_falls_back(pkg, cuda):
+    """A scene whose visible depths clump into one MSD bucket (> 16384
+    Gaussians at nearly the same depth) renders exactly as with the LSD depth
+    sort: the overflow poisons the frame's depth max, the frame is sorted
+    again, and the LSD path is kept for the next frames."""
+    from mini3dgs_amd import rasterizer as RZ
+    rng = np.random.default_rng(5)
+    n, W, H = 60_000, 320, 240
+    scene = pkg.synthetic.make_scene(n, W, H, seed=3)
+    model = pkg.synthetic.to_model(scene, pkg.GaussianModel, cuda)
+    with torch.no_grad():
+        z = torch.tensor(rng.uniform(2, 6, n), dtype=torch.float32, device=cuda)
+        z[: n // 2] = 3.0 + torch.arange(n // 2, device=cuda, dtype=torch.float32) * 1e-7  # a depth clump
+        model._xyz[:, :2] *= (z / model._xyz[:, 2])[:, None]
+        model._xyz[:, 2] = z
+    cam = Cam(W, H, scene.fovx, scene.fovy)
+    st = pkg.RenderSettings(image_height=H, image_width=W, bg_color=torch.zeros(3))
+    r = pkg.GaussianRenderer()
+    RZ._MSD_BACKOFF.clear()
+    try:
+        with torch.no_grad():
+            outs = [r.render(cam, model, st)["image"].clone() for _ in range(3)]  # windowed keys + overflow
+            assert RZ._MSD_BACKOFF.get(model._xyz.device, 0) > 0, "the clump must overflow an MSD bucket"
+            RZ._DEPTH_MSD = False
+            ref = r.render(cam, model, st)["image"]
+    finally:
+        RZ._DEPTH_MSD = True
+        RZ._MSD_BACKOFF.clear()
+    for o in outs:
+        assert torch.equal(o, ref)
+
+
 def test_forward_capacity_paths(pkg, cuda):
     """The forward queues the emission before the T read-back into buffers
     sized from the last frame's T (+ 25 %); a frame whose T outgrows that
