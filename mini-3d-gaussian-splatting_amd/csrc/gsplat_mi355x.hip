@@ -629,13 +629,15 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__res
   // wave w: items [w seg, (w + 1) seg), seg a multiple of 64; order (wave, round, lane)
   const uint32_t seg = (size + kMsdThreads - 1) / kMsdThreads * kWave;
   const int rounds = (int)(seg / kWave);
+  // every round's key and value requested at once: unconditional loads of a
+  // clamped index (a load under a branch is waited for at its join)
   uint32_t k_[kMsdIpt], v_[kMsdIpt];
 #pragma unroll
   for (int r = 0; r < kMsdIpt; ++r) {
     const uint32_t i = (uint32_t)wave * seg + (uint32_t)(r * kWave + lane);
-    const bool ok = r < rounds && i < size;
-    k_[r] = ok ? keys[start + i] : 0u;
-    v_[r] = ok ? vals[start + i] : 0u;
+    const uint32_t ic = (r < rounds && i < size) ? i : 0u;
+    k_[r] = keys[start + ic];
+    v_[r] = vals[start + ic];
   }
   const int passes = (lowbits + kRadixBits - 1) / kRadixBits;
   int shift = 0;
@@ -700,10 +702,9 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__res
 #pragma unroll
       for (int r = 0; r < kMsdIpt; ++r) {
         const uint32_t i = (uint32_t)wave * seg + (uint32_t)(r * kWave + lane);
-        if (r < rounds && i < size) {
-          k_[r] = s_k[i];
-          v_[r] = s_v[i];
-        }
+        const uint32_t ic = (r < rounds && i < size) ? i : 0u;  // (unconditional, as above)
+        k_[r] = s_k[ic];
+        v_[r] = s_v[ic];
       }
     }
   }
