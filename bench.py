@@ -10,7 +10,9 @@ gradients -> Adam step.  Each step first restores the parameters from a
 snapshot (a multi-tensor copy inside the timed region) so that every timed
 frame renders the same scene.  Rank r renders view r of the same replicated 1M
 Gaussian model (weak scaling: one 1080p view per GPU per step).  Inputs are
-resident in HBM before the timed region.  `value` = all ranks' pixels /
+resident in HBM before the timed region.  Before the W warm-up steps,
+--spinup-steps (default 50, reported in the line) untimed steps bring the GPU
+to its steady clock.  `value` = all ranks' pixels /
 max-over-ranks step time.
 
 Also reported: the roofline of the dominant kernel (HIP events on the
@@ -57,6 +59,11 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--no-optimizer", action="store_true", help="time render fwd+bwd only")
     ap.add_argument("--diag-steps", type=int, default=5, help="untimed steps for the per-stage breakdown")
+    # MI355X clocks ramp over the first ~60 ms of load: with 5 warm-up steps the
+    # timed steps ran 1.25 ms, with 50 or 200 1.19 (same box, profiles/r02/warmup.log).
+    # A fixed count (not a time) so that every rank runs the same collectives.
+    ap.add_argument("--spinup-steps", type=int, default=50,
+                    help="untimed steps before the --warmup steps, for the GPU clock ramp")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="oracle threads (capped by the CPUs this process may run on); the box's share is 16")
@@ -182,7 +189,7 @@ def main():
             opt.step()
         frames.append(out)
 
-    for _ in range(a.warmup):
+    for _ in range(a.spinup_steps + a.warmup):
         step()
         frames.clear()
     if dist is not None:
@@ -287,7 +294,7 @@ def main():
                            "pinned to the reference's own outputs); db None = bit-identical images"}
         line = {
             "metric": METRIC, "value": round(mpix, 3), "unit": "Mpix/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup": a.warmup, "spinup_steps": a.spinup_steps, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C3: 1M synthetic Gaussians (SURVEY 8d), 1920x1080, 16x16 tiles, "
                                    "render fwd+bwd" + ("" if opt is None else " + grad all-reduce + Adam step"),
