@@ -62,6 +62,8 @@ def parse():
     # MI355X clocks ramp over the first ~60 ms of load: with 5 warm-up steps the
     # timed steps ran 1.25 ms, with 50 or 200 1.19 (same box, profiles/r02/warmup.log).
     # A fixed count (not a time) so that every rank runs the same collectives.
+    ap.add_argument("--view", type=int, default=None,
+                    help="render rank R's view (diagnostics; default: this rank's own)")
     ap.add_argument("--spinup-steps", type=int, default=50,
                     help="untimed steps before the --warmup steps, for the GPU clock ramp")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -157,7 +159,7 @@ def main():
         [{"params": [model._xyz], "lr": 1.6e-4}, {"params": [model._features_dc], "lr": 2.5e-3},
          {"params": [model._opacity], "lr": 0.05}, {"params": [model._scaling], "lr": 5e-3},
          {"params": [model._rotation], "lr": 1e-3}])
-    cam = BenchCamera(W, H, scene.fovx, scene.fovy, view_matrix(rank))
+    cam = BenchCamera(W, H, scene.fovx, scene.fovy, view_matrix(rank if a.view is None else a.view))
     settings = pkg.RenderSettings(image_height=H, image_width=W, bg_color=torch.zeros(3))
     renderer = pkg.GaussianRenderer()
     g = torch.Generator().manual_seed(1)

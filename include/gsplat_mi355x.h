@@ -153,7 +153,7 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
                               size_t workspace_bytes, int32_t *result_in_alt,
                               gs_stream_t stream);
 
-/* Windowed depth keys (9 <= key_bits <= 24, gs_project_args.key_bits): the
+/* Windowed depth keys (9 <= key_bits <= 32, gs_project_args.key_bits): the
  * same result as gs_radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, 0,
  * key_bits, 1, ...) -- values = input positions, stable -- in one 8-bit MSD
  * pass plus one LDS-resident sort per top-digit bucket (one workgroup each).
@@ -163,8 +163,9 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
  * 16384 keys is left unsorted and 0xFFFFFFFF is stored to *overflow_word
  * (renderer: the depth-max word of gs_project_args.key_minmax, so the frame's
  * window check fails and it is sorted again with gs_radix_sort_pairs).
- * Workspace: gs_radix_sort_workspace_bytes(n).  key_bits outside 9..24
- * returns GS_ERR_UNSUPPORTED. */
+ * The buckets are sorted by the low key_bits - 8 bits in ceil((key_bits - 8)
+ * / 8) LDS passes.  Workspace: gs_radix_sort_workspace_bytes(n).  key_bits
+ * outside 9..32 returns GS_ERR_UNSUPPORTED. */
 gs_status gs_depth_sort_msd(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
                             int32_t n, int32_t key_bits, void *workspace, size_t workspace_bytes,
                             uint32_t *overflow_word, int32_t *result_in_alt, gs_stream_t stream);

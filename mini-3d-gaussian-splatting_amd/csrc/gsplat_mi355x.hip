@@ -2033,8 +2033,8 @@ gs_status gs_depth_sort_msd(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, 
                             int32_t key_bits, void *workspace, size_t workspace_bytes, uint32_t *overflow_word,
                             int32_t *result_in_alt, gs_stream_t stream) {
   if (!result_in_alt) return fail(GS_ERR_INVALID_ARG, "%s: null result_in_alt", "gs_depth_sort_msd");
-  if (key_bits < 9 || key_bits > 24 || n < 0)
-    return fail(GS_ERR_UNSUPPORTED, "%s: key_bits must be 9..24", "gs_depth_sort_msd");
+  if (key_bits < 9 || key_bits > 32 || n < 0)
+    return fail(GS_ERR_UNSUPPORTED, "%s: key_bits must be 9..32", "gs_depth_sort_msd");
   *result_in_alt = 1;
   if (n == 0) return GS_OK;
   if (!keys || !vals || !keys_alt || !vals_alt || !workspace || !overflow_word ||

@@ -157,7 +157,7 @@ _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess
 _HOST_COUNTERS = threading.local()
 _FUSE_FLAGS = os.environ.get("GS_FUSE_SLOT_FLAGS", "1") != "0"  # slot flags zeroed by gs_tile_ranges
 _DEPTH_WINDOW: dict = {}  # device -> (key_base, key_bits) from its last frame's visible depth range
-# Windowed depth keys of 9..24 bits are sorted by gs_depth_sort_msd (one MSD pass + a sort per
+# Windowed depth keys of 9..31 bits are sorted by gs_depth_sort_msd (one MSD pass + a sort per
 # bucket in LDS) unless GS_DEPTH_MSD=0.  A bucket over its LDS capacity (clumped depths) poisons
 # the frame's depth max (0xFFFFFFFF): the frame is sorted again with the LSD passes, and the LSD
 # path is kept for the next _MSD_BACKOFF_FRAMES frames on that device.
@@ -170,7 +170,9 @@ _POISON = 0xFFFFFFFF
 def depth_window(zmin_bits: int, zmax_bits: int):
     """(key_base, key_bits) of a window around the visible fp32 depth bits
     [zmin_bits, zmax_bits], widened by 1/8 of the range on both sides for the
-    next frame's drift; None when no pass would be saved (32 bits anyway)."""
+    next frame's drift; None when the range needs all 32 bits.  Windows of 25-31
+    bits save no LSD pass, but they keep the depth sort on gs_depth_sort_msd
+    (raw fp32 bits would put every key into one MSD bucket)."""
     if zmin_bits > zmax_bits:
         return None
     span = zmax_bits - zmin_bits
@@ -179,7 +181,7 @@ def depth_window(zmin_bits: int, zmax_bits: int):
     bits = max(1, (hi - lo + 1).bit_length())  # keys 0 .. hi - lo < 2^bits - 1 (the culled sentinel)
     if bits >= 9 and hi - lo >= _msd_limit(bits):
         bits += 1  # the MSD depth sort's top bucket is the sentinel's alone
-    return (lo, bits) if (bits + 7) // 8 < 4 else None
+    return (lo, bits) if bits < 32 else None
 
 
 def _msd_limit(bits: int) -> int:
@@ -280,7 +282,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         backoff = _MSD_BACKOFF.get(dev, 0)
         if backoff:
             _MSD_BACKOFF[dev] = backoff - 1
-        if _DEPTH_MSD and window is not None and 9 <= key_bits <= 24 and not backoff:
+        if _DEPTH_MSD and window is not None and 9 <= key_bits <= 31 and not backoff:
             N.check(lib.gs_depth_sort_msd(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n,
                                           key_bits, N.ptr(ws), ws.numel(), N.ptr(key_minmax) + 4, C.byref(alt),
                                           s), "depth sort (msd)")

@@ -242,7 +242,8 @@ def test_depth_sort_msd_matches_stable_argsort(pkg, cuda):
     # (n, bits, culled fraction, clumped): clumped = every visible key in two buckets
     for n, bits, culled, clump in ((1, 9, 0.0, False), (5, 12, 0.4, False), (1000, 9, 0.1, False),
                                    (100_000, 16, 0.0, False), (1_000_000, 24, 0.0, False),
-                                   (300_000, 20, 0.5, False), (40_000, 24, 0.0, True), (2049, 17, 1.0, False)):
+                                   (300_000, 20, 0.5, False), (40_000, 24, 0.0, True), (2049, 17, 1.0, False),
+                                   (600_000, 25, 0.1, False), (200_000, 28, 0.2, False), (100_000, 32, 0.0, False)):
         lim = 255 << (bits - 8)
         if clump:
             k = (rng.integers(0, 2, n) << (bits - 8)) + rng.integers(0, 50, n)  # ~20k keys per bucket
@@ -269,7 +270,7 @@ def test_depth_sort_msd_matches_stable_argsort(pkg, cuda):
         assert np.array_equal(vv[1].cpu().numpy().view(np.uint32), order.astype(np.uint32)), (n, bits)
         assert np.array_equal(kk[1].cpu().numpy().view(np.uint32), k[order]), (n, bits)
     with pytest.raises(RuntimeError):
-        N.check(lib.gs_depth_sort_msd(N.ptr(kk[0]), N.ptr(vv[0]), N.ptr(kk[1]), N.ptr(vv[1]), 10, 32, N.ptr(ws),
+        N.check(lib.gs_depth_sort_msd(N.ptr(kk[0]), N.ptr(vv[0]), N.ptr(kk[1]), N.ptr(vv[1]), 10, 33, N.ptr(ws),
                                       ws.numel(), N.ptr(flag), C.byref(alt), None), "msd sort")
 
 

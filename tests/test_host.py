@@ -112,7 +112,8 @@ def test_synthetic_scene_distribution(pkg):
 def test_depth_window_choice(pkg):
     """rasterizer.depth_window: a window of key bits around the previous
     frame's visible fp32 depth bits, widened by 1/8 of the range each side;
-    None when it would not save a radix pass."""
+    None when the range needs all 32 bits.  Visible keys stay below
+    255 << (bits - 8): the MSD depth sort's top bucket is the culled sentinel's."""
     import struct
     RZ = pkg.rasterizer
     bits = lambda z: struct.unpack("<I", struct.pack("<f", z))[0]
@@ -120,7 +121,9 @@ def test_depth_window_choice(pkg):
     assert w is not None and w[1] <= 24
     assert RZ.window_holds(w, bits(2.0), bits(6.0)) and RZ.window_holds(w, bits(2.1), bits(5.5))
     assert not RZ.window_holds(w, bits(0.5), bits(6.0)) and not RZ.window_holds(w, bits(2.0), bits(60.0))
-    assert RZ.depth_window(bits(0.01), bits(1000.0)) is None  # > 24 bits: no pass saved
+    w = RZ.depth_window(bits(0.01), bits(1000.0))  # 28 bits: no LSD pass saved, but the MSD sort's
+    assert w is not None and 24 < w[1] < 32 and RZ.window_holds(w, bits(0.01), bits(1000.0))
+    assert RZ.depth_window(bits(1e-38), bits(3e38)) is None  # all 32 bits
     assert RZ.depth_window(0xFFFFFFFF, 0) is None  # nothing visible
     assert RZ.window_holds(None, bits(0.01), bits(1e30))
     base, nb = RZ.depth_window(bits(3.0), bits(3.0))  # a single depth
