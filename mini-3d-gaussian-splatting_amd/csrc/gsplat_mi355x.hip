@@ -28,6 +28,9 @@ constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
+#ifndef GS_HIST_DIRECT_ATOMICS  // radix histogram: 1 = one LDS atomic per key, 0 = ballot-matched digits
+#define GS_HIST_DIRECT_ATOMICS 1
+#endif
 #ifndef GS_SORT_IPT
 #define GS_SORT_IPT 8
 #endif
@@ -447,6 +450,14 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restric
     const long long idx = base + r * 64 + lane;
     kr[r] = keys[idx < n ? idx : n - 1];
   }
+#if GS_HIST_DIRECT_ATOMICS
+  // one LDS atomic per key (the LDS serialises equal addresses itself)
+#pragma unroll
+  for (int r = 0; r < kSortIpt; ++r) {
+    const long long idx = base + r * 64 + lane;
+    if (idx < n) atomicAdd(&hist[(kr[r] >> shift) & mask], 1u);
+  }
+#else
 #pragma unroll
   for (int r = 0; r < kSortIpt; ++r) {
     const long long idx = base + r * 64 + lane;
@@ -455,6 +466,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restric
     const unsigned long long m = match_digit(d, nbits, __ballot(valid));
     if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(m));
   }
+#endif
   __syncthreads();
   if (threadIdx.x <= mask) counts[(size_t)threadIdx.x * nb + blockIdx.x] = hist[threadIdx.x];
 }
