@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 11
+#define GS_ABI_VERSION 12
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
@@ -43,7 +43,7 @@ extern "C" {
                                  ceil((2 floor(radius_max) + 1) / L) + 1 <= 256;
                                  gs_project_forward returns GS_ERR_UNSUPPORTED otherwise */
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
-#define GS_PAIR_GRAD_FLOATS 10 /* per (tile, Gaussian, 8x8 cell) gradient partial */
+#define GS_PAIR_GRAD_FLOATS 10 /* per (list entry, partial group) gradient partial (gs_partial_groups) */
 #define GS_PARTIAL_STRIDE 10   /* floats between partials in pair_grads (dense: 40 B each) */
 #define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2] / [3] min / max fp32 bits of the
                                  visible depths (0xFFFFFFFF / 0 when none; see gs_project_args) */
@@ -215,7 +215,7 @@ typedef struct gs_range_args {
   uint32_t *ranges;            /* [num_tiles,2] */
   uint8_t *slot_live;          /* optional (NULL: none): zeroed here, [T, cells] -- the backward's
                                   gs_blend_bwd_args.slot_live, cleared without a kernel of its own */
-  int32_t cells;               /* gs_tile_quads(tile_size), with slot_live */
+  int32_t cells;               /* gs_partial_groups(tile_size), with slot_live */
 } gs_range_args;
 gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream);
 
@@ -255,17 +255,24 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
 size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles);
 /* Cells per tile: ceil(tile_size / 8)^2 (4 for the default 16); 0 if out of range. */
 int32_t gs_tile_quads(int32_t tile_size);
+/* Gradient partials gs_blend_backward writes per list entry (G below): 1 for
+ * the default 16x16 tile, whose backward waves add the four cells' sums of an
+ * entry on chip; gs_tile_quads(tile_size) for every other tile size (one per
+ * cell); 0 if out of range. */
+int32_t gs_partial_groups(int32_t tile_size);
 
 /* ---- Backward of the blend -------------------------------------------
- * One 64-lane workgroup per (tile, 8x8 cell), independent of the others:
- * re-walks each pixel's list front-to-back (bit-identical replay of the
+ * Re-walks each pixel's list front-to-back (bit-identical replay of the
  * forward's decisions) over the entries the forward's liveness bitmap marks
- * for the cell, and writes one partial gradient per (entry, cell):
- * pair_grads[Q e + q] = {dmu_x, dmu_y, dQ00, dQ01(=dQ10), dQ11, d_opacity,
- * d_r, d_g, d_b, d_z} over cell q's pixels, and sets slot_live[Q e + q] = 1;
- * Q = gs_tile_quads(tile_size), e = the entry's gradient slot (pair_offset[g]
- * + its tile's index in g's rectangle).  Partials of cells that did not
- * replay the entry are not written.  No atomics: deterministic. */
+ * for its 8x8 cell, and writes one partial gradient per (entry, partial
+ * group): pair_grads[G e + q] = {dmu_x, dmu_y, dQ00, dQ01(=dQ10), dQ11,
+ * d_opacity, d_r, d_g, d_b, d_z} summed over group q's pixels, and sets
+ * slot_live[G e + q] = 1; G = gs_partial_groups(tile_size), e = the entry's
+ * gradient slot (pair_offset[g] + its tile's index in g's rectangle).  At the
+ * default tile one 64-lane workgroup replays a whole 16x16 tile (its four
+ * cells in turn, word by word) and G = 1; otherwise one workgroup per (tile,
+ * cell) and the group is the cell.  Groups that did not replay the entry
+ * write nothing.  No atomics: deterministic. */
 typedef struct gs_blend_bwd_args {
   gs_camera cam;
   int32_t tiles_x, tiles_y;
@@ -279,14 +286,14 @@ typedef struct gs_blend_bwd_args {
   const float *g_depth;         /* [H,W] or NULL */
   const uint64_t *live_bits;    /* the forward's liveness bitmap */
   int64_t live_words;
-  float *pair_grads;            /* [T, Q, GS_PARTIAL_STRIDE], Q = gs_tile_quads(cam.tile_size) */
-  uint8_t *slot_live;           /* [T, Q], zeroed by the caller */
+  float *pair_grads;            /* [T, G, GS_PARTIAL_STRIDE], G = gs_partial_groups(cam.tile_size) */
+  uint8_t *slot_live;           /* [T, G], zeroed by the caller (or gs_tile_ranges) */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
 
 /* ---- Backward of the projection ----------------------------------------
  * Sums each Gaussian's slot partials (slots [pair_offset[g], pair_offset[g]
- * + touches), the cells slot_live flags), adds cotangents on the viewspace_points /
+ * + touches), the groups slot_live flags), adds cotangents on the viewspace_points /
  * conics outputs, and chains through sigmoid(colour), inv(cov2d),
  * J cov_cam J^T, Rv Sigma Rv^T, the perspective Jacobian J(X,Y,Z) and
  * Xc = Rv Xw + Tv (autograd of renderer.py:117-200), and, on the raw path,
@@ -302,7 +309,7 @@ typedef struct gs_project_bwd_args {
   const uint32_t *pair_offset;
   const uint32_t *order;       /* [n] permutation to walk the Gaussians in, or NULL: index order
                                   (slots are numbered in index order, so NULL reads them coalesced) */
-  const float *pair_grads;     /* [T,Q,GS_PARTIAL_STRIDE]; may be NULL when T == 0 */
+  const float *pair_grads;     /* [T,G,GS_PARTIAL_STRIDE] (gs_partial_groups); may be NULL when T == 0 */
   const float *g_means2d;      /* [n,2] or NULL */
   const float *g_conics;       /* [n,4] or NULL */
   float *d_xyz;                /* [n,3] */
@@ -312,7 +319,7 @@ typedef struct gs_project_bwd_args {
   float *d_color_logits;       /* [n,3] */
   float *d_opacity;            /* [n]   */
   float *d_sh_rest;            /* [n,15,3] contiguous, written when g.sh_degree > 0 (zeros past the degree) */
-  const uint8_t *slot_live;    /* [T,Q] from gs_blend_backward; required with pair_grads */
+  const uint8_t *slot_live;    /* [T,G] from gs_blend_backward; required with pair_grads */
   float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS] scratch (g's partials summed); with pair_grads */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);

@@ -25,9 +25,9 @@ GS_MAX_TILE = 256
 GS_QUAD = 8  # 8x8 pixel cells per wave, ceil(tile/8)^2 per tile (gs_tile_quads)
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
-GS_PARTIAL_STRIDE = 10  # floats between cell partials in pair_grads (dense)
+GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 11
+GS_ABI_VERSION = 12
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -156,7 +156,7 @@ class GsDensifyArgs(C.Structure):
 EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
-    "gs_tile_ranges", "gs_blend_live_words", "gs_tile_quads", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
+    "gs_tile_ranges", "gs_blend_live_words", "gs_tile_quads", "gs_partial_groups", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
     "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
     "gs_densify_workspace_bytes", "gs_densify_count", "gs_densify_emit",
 )
@@ -189,6 +189,8 @@ def _declare(lib):
     lib.gs_blend_live_words.restype = C.c_size_t
     lib.gs_tile_quads.argtypes = [C.c_int32]
     lib.gs_tile_quads.restype = C.c_int32
+    lib.gs_partial_groups.argtypes = [C.c_int32]
+    lib.gs_partial_groups.restype = C.c_int32
     lib.gs_blend_forward.argtypes = [P(GsBlendFwdArgs), _vp]
     lib.gs_blend_backward.argtypes = [P(GsBlendBwdArgs), _vp]
     lib.gs_project_backward.argtypes = [P(GsProjectBwdArgs), _vp]

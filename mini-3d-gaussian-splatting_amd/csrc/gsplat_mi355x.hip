@@ -80,6 +80,14 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) {
   return v < lo ? lo : (v > hi ? hi : v);
 }
 
+// Dense 40-B gradient partials are 8-B aligned only: 16-B accesses to them go
+// through this explicitly under-aligned vector type (global_load/store_dwordx4
+// need 4-B alignment on gfx950; a plain float4 would promise 16).  Five
+// float2 accesses instead cost the gather ~35 us at C3 (more load
+// instructions in flight per partial).
+typedef float f4_u8 __attribute__((ext_vector_type(4), aligned(8)));
+typedef float f2_u8 __attribute__((ext_vector_type(2), aligned(8)));
+
 // exp(x) for the blend's range x in [-11.6, 0] (it evaluates exp(-s/2) only
 // for s <= 23.1): x*log2(e) split into ph + pl (Cody-Waite, as ocml's expf),
 // then 2^ph by v_exp_f32 corrected by (1 + pl ln2) -- no range reduction and
@@ -975,6 +983,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
   if (a.slot_live && p < a.num_pairs) {  // slot p's flags for the backward (coalesced)
     if (a.cells == 4)
       reinterpret_cast<uint32_t *>(a.slot_live)[p] = 0u;
+    else if (a.cells == 1)
+      a.slot_live[p] = 0;
     else
       for (int c = 0; c < a.cells; ++c) a.slot_live[p * a.cells + c] = 0;
   }
@@ -1120,6 +1130,8 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
     unsigned long long m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mw >> 32)) << 32) |
                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mw);
     // the next batch's records in flight while this one composites
+    // (fetching the ids a batch earlier, so that this is one round trip, was
+    // measured: no change, profiles/r03/experiments.md)
     if (b + kWave + (uint32_t)lane < end) {
       const uint32_t gid = a.sorted_gauss[b + kWave + lane];
       n0 = recs[3 * (size_t)gid];
@@ -1397,10 +1409,11 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
         const size_t sq = (size_t)slot * (uint32_t)ncell + (uint32_t)quad;
-        float4 *out = reinterpret_cast<float4 *>(a.pair_grads + sq * GS_PARTIAL_STRIDE);
-        out[0] = make_float4(g0, g1, g2, g3);
-        out[1] = make_float4(g4, g5, g6, g7);
-        *reinterpret_cast<float2 *>(out + 2) = make_float2(g8, g9);
+        // (dense 40-B partials, 8-B aligned: f4_u8)
+        float *out = a.pair_grads + sq * GS_PARTIAL_STRIDE;
+        *reinterpret_cast<f4_u8 *>(out) = f4_u8{g0, g1, g2, g3};
+        *reinterpret_cast<f4_u8 *>(out + 4) = f4_u8{g4, g5, g6, g7};
+        *reinterpret_cast<f2_u8 *>(out + 8) = f2_u8{g8, g9};
         a.slot_live[sq] = 1;
       }
     }
@@ -1539,19 +1552,363 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   }
 }
 
+// ============================================ blend bwd, combined cells ===
+// The default 16x16 tile: one wave takes kBwdCpw of the tile's four 8x8
+// cells (4: the whole tile, 2: a 16x8 half) and replays them word by word --
+// for each 64-entry word of the tile's list, its cells in turn, each over its
+// own liveness bits with its own pixel chains exactly as k_blend_bwd does
+// for one cell -- and adds the cells' phase-B sums of an entry in registers
+// (lane = the entry's bit in the word, cells in a fixed order) before
+// anything leaves the chip: one partial per (entry, group of kBwdCpw cells)
+// instead of one per (entry, cell), so the partial stores and the gather's
+// reads shrink by the cells an entry reaches on average (2.6 at C3).  A
+// cell's per-pixel state rotates through cs[0]: the per-cell body is not
+// unrolled (code size), the rotation costs a few moves per (word, cell).
+#ifndef GS_BWD_CPW
+#define GS_BWD_CPW 1
+#endif
+constexpr int kBwdCpw = GS_BWD_CPW;
+static_assert(kBwdCpw == 1 || kBwdCpw == 2 || kBwdCpw == 4, "cells per backward wave: 1, 2 or 4");
+
+// One pixel's backward state in one cell.
+struct BwdPixel {
+  float gR0, gR1, gR2, gD, gA;  // cotangents through clamp / bg composite / depth normalisation
+  float A, T1, PG;              // the replay: A, 1 - A (carried), P + G0 (see k_blend_bwd)
+  uint32_t neval;               // entries the forward evaluated for this pixel
+};
+
+template <int CPW>
+__global__ __launch_bounds__(kWave) void k_blend_bwd_grp(gs_blend_bwd_args a) {
+  __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
+  __shared__ float4 s_pg[kWave];               // the current cell's pixels: dL/drgb (masked), dL/dD
+  __shared__ float2 s_wrec[kBwdGroup * 6];     // the chunk's records (word 10 = slot)
+  constexpr int NG = 4 / CPW;                  // partial groups per tile
+  const int ntiles = a.tiles_x * a.tiles_y;
+  // workgroup b -> (tile, group): the XCD b & 7 (round-robin dispatch) takes
+  // the row-major band of tiles [x per, (x + 1) per), so neighbouring tiles,
+  // which share Gaussians, read records through one L2 (speed only)
+  const uint32_t per = ((uint32_t)ntiles + 7u) >> 3, kq = blockIdx.x >> 3;
+  const int grp = (int)(kq % (uint32_t)NG);
+  const int tile = (int)((blockIdx.x & 7u) * per + kq / (uint32_t)NG);
+  if (tile >= ntiles) return;
+  const int lane = threadIdx.x;
+  const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
+  const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]);
+  const uint32_t lend = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
+  if (start >= lend) return;
+  const float4 *recs = reinterpret_cast<const float4 *>(a.records);
+  const int W = a.cam.image_width, H = a.cam.image_height;
+  const size_t HW = (size_t)W * H;
+  const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
+  // the prologue's loads in two round trips, unconditionally (k_blend_bwd):
+  // every cell's pixel state and cotangents and word-0 liveness word, the
+  // word-0 entries' ids; then speculatively every word-0 entry's record
+  const unsigned long long *lwb = reinterpret_cast<const unsigned long long *>(a.live_bits);
+  const size_t lw_off = start / 64u + (uint32_t)tile;
+  unsigned long long w0[CPW];
+  float4 accp[CPW];
+  float2 stp[CPW];
+  float gip[CPW][5];
+  bool inside[CPW];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) {
+    const int c = grp * CPW + i;
+    const int px = (int)tx * 16 + (c & 1) * 8 + (lane & 7), py = (int)ty * 16 + (c >> 1) * 8 + (lane >> 3);
+    inside[i] = px < W && py < H;
+    const size_t p = inside[i] ? (size_t)py * W + px : 0;
+    w0[i] = lwb[(size_t)c * a.live_words + lw_off];
+    accp[i] = reinterpret_cast<const float4 *>(a.pix_acc)[p];
+    stp[i] = reinterpret_cast<const float2 *>(a.pix_state)[p];
+    gip[i][0] = a.g_image[p];
+    gip[i][1] = a.g_image[HW + p];
+    gip[i][2] = a.g_image[2 * HW + p];
+    gip[i][3] = (a.g_alpha ? a.g_alpha : a.g_image)[p];
+    gip[i][4] = (a.g_depth ? a.g_depth : a.g_image)[p];
+  }
+  const uint32_t gid0 = a.sorted_gauss[start + (uint32_t)lane < lend ? start + (uint32_t)lane : 0u];
+  float4 r0 = recs[3 * (size_t)gid0], r1 = recs[3 * (size_t)gid0 + 1], r2 = recs[3 * (size_t)gid0 + 2];
+  BwdPixel cs[CPW];
+  uint32_t nwords[CPW], wstop[CPW];
+  uint32_t nw = 0;
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) {
+    // pixel cotangents (k_blend_bwd; selects, no branch)
+    const bool in = inside[i];
+    const float tr = in ? accp[i].x : 0.f, tg = in ? accp[i].y : 0.f, tbl = in ? accp[i].z : 0.f;
+    const float Dt = in ? accp[i].w : 0.f, At = in ? stp[i].x : 0.f;
+    const float tb = 1.f - At;
+    const float pr = tr + tb * bg0, pg = tg + tb * bg1, pb = tbl + tb * bg2;
+    BwdPixel &P = cs[i];
+    P.gR0 = (in && pr >= 0.f && pr <= 1.f) ? gip[i][0] : 0.f;
+    P.gR1 = (in && pg >= 0.f && pg <= 1.f) ? gip[i][1] : 0.f;
+    P.gR2 = (in && pb >= 0.f && pb <= 1.f) ? gip[i][2] : 0.f;
+    float gA = -P.gR0 * bg0 - P.gR1 * bg1 - P.gR2 * bg2;
+    if (in && a.g_alpha && At >= 0.f && At <= 1.f) gA += gip[i][3];
+    const bool has_d = in && a.g_depth;
+    const float den = At + 1e-6f;
+    P.gD = has_d ? gip[i][4] / den : 0.f;
+    const float gAd = -gip[i][4] * Dt / (den * den);
+    if (has_d) gA += gAd;
+    P.gA = gA;
+    P.neval = in ? __float_as_uint(stp[i].y) : 0u;
+    const float K = (P.gR0 * tr + P.gR1 * tg) + (P.gR2 * tbl + P.gD * Dt);
+    const float G0 = __builtin_fmaf(gA, 1.f - At, -K);
+    P.PG = ((P.gR0 * bg0 + P.gR1 * bg1) + P.gR2 * bg2) + G0;
+    P.A = 0.f;
+    P.T1 = 1.f;
+    wstop[i] = __builtin_amdgcn_readfirstlane(wave_max_u32(P.neval));
+    nwords[i] = (wstop[i] + 63u) >> 6;
+    nw = nw > nwords[i] ? nw : nwords[i];
+  }
+  if (nw == 0) return;
+  // liveness word wd of cell i, cut at the cell's last evaluated entry (bits
+  // past it were never written; words past it are not read)
+  auto live_word = [&](int i, uint32_t wd) -> unsigned long long {
+    if (wd >= nwords[i]) return 0ull;
+    const unsigned long long w = wd == 0 ? w0[i] : lwb[(size_t)(grp * CPW + i) * a.live_words + lw_off + wd];
+    const unsigned long long m =
+        ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)w);
+    const uint32_t rem = wstop[i] - 64u * wd;
+    return rem < 64u ? m & ((1ull << rem) - 1ull) : m;
+  };
+  unsigned long long mc[CPW];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) mc[i] = live_word(i, 0);
+  const int j = lane / kBwdLanes, sub = lane % kBwdLanes, col = sub & 7, row0 = sub >> 3;
+  for (uint32_t wd = 0; wd < nw; ++wd) {
+    unsigned long long U = 0;
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) U |= mc[i];
+    const bool mineU = (U >> lane) & 1ull;
+    // word 10 of a live record becomes the entry's gradient slot
+    const uint32_t info = __float_as_uint(r2.w);
+    const uint32_t slot = __float_as_uint(r2.z) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
+                          (tx - (info & 0xFFFu));
+    const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
+    const unsigned long long simple_w = __builtin_amdgcn_ballot_w64(mineU && simple_entry(r0, r1));
+    unsigned long long mn[CPW], Un = 0;
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+      mn[i] = live_word(i, wd + 1u);
+      Un |= mn[i];
+    }
+    if ((Un >> lane) & 1ull) {  // the next word's records, in flight while this word replays
+      const uint32_t gid = a.sorted_gauss[start + 64u * (wd + 1u) + (uint32_t)lane];
+      r0 = recs[3 * (size_t)gid];
+      r1 = recs[3 * (size_t)gid + 1];
+      r2 = recs[3 * (size_t)gid + 2];
+    }
+    // this word's entries' partials summed over the cells; lane = entry bit
+    float acc[GS_PAIR_GRAD_FLOATS];
+#pragma unroll
+    for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
+#pragma unroll 1
+    for (int i = 0; i < CPW; ++i) {
+      const unsigned long long mcell = mc[0];
+      if (mcell) {
+        BwdPixel &P = cs[0];
+        const int c = grp * CPW + i;
+        const int x0 = (int)tx * 16 + (c & 1) * 8, y0 = (int)ty * 16 + (c >> 1) * 8;
+        const float fx = (float)(x0 + (lane & 7)), fy = (float)(y0 + (lane >> 3));
+        // (the previous cell's phase-B reads precede this write in the wave's LDS queue)
+        s_pg[lane] = make_float4(P.gR0, P.gR1, P.gR2, P.gD);
+        const bool mine = (mcell >> lane) & 1ull;
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(mcell >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mcell, 0u));
+        // Phase B over a chunk of k live entries (k_blend_bwd), the sums then
+        // moved to the lanes of their word bits and added to acc
+        auto phase_b = [&](auto masked_tag, unsigned long long cm, int k) {
+          constexpr bool kMasked = decltype(masked_tag)::value;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the group buffer rows
+          float v[GS_PAIR_GRAD_FLOATS];
+#pragma unroll
+          for (int q = 0; q < GS_PAIR_GRAD_FLOATS; ++q) v[q] = 0.f;
+          if (j < k) {
+            const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * j];  // mx my q00 q11
+            const float2 ib = s_wrec[6 * j + 2];                                // qo o
+            const float hop = -0.5f * ib.y;
+            const float bx = (float)(x0 + col) - ia.x, by = (float)(y0 + row0) - ia.y;
+            float S0 = 0.f, Soy = 0.f, Soyy = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
+#pragma unroll
+            for (int r = 0; r < kBwdGroup; ++r) {
+              const int p = col + 8 * (row0 + kBwdStep * r);
+              const float2 dc = s_dc[j][p];
+              const float dop = dc.x, csg = dc.y;
+              const float4 pg = s_pg[p];
+              const float ds = kMasked ? (csg > 0.f ? hop * dop : 0.f) : hop * dop;
+              const float cw = fabsf(csg);
+              S0 += ds;
+              if (r) {
+                Soy = __builtin_fmaf(ds, (float)(kBwdStep * r), Soy);
+                Soyy = __builtin_fmaf(ds, (float)(kBwdStep * kBwdStep * r * r), Soyy);
+              }
+              g5 += dop;
+              g6 = __builtin_fmaf(pg.x, cw, g6);
+              g7 = __builtin_fmaf(pg.y, cw, g7);
+              g8 = __builtin_fmaf(pg.z, cw, g8);
+              g9 = __builtin_fmaf(pg.w, cw, g9);
+            }
+            float Sx = bx * S0, Sy = __builtin_fmaf(by, S0, Soy);
+            float g2 = bx * Sx, g3 = bx * Sy;
+            float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
+            auto red = [](float x) { return kBwdLanes == 8 ? oct_sum(x) : row16_sum(x); };
+            Sx = red(Sx); Sy = red(Sy); g2 = red(g2); g3 = red(g3); g4 = red(g4);
+            g5 = red(g5); g6 = red(g6); g7 = red(g7); g8 = red(g8); g9 = red(g9);
+            const float q00 = ia.z, qo = ib.x, q11 = ia.w;
+            v[0] = -(2.f * q00 * Sx + qo * Sy);
+            v[1] = -(qo * Sx + 2.f * q11 * Sy);
+            v[2] = g2; v[3] = g3; v[4] = g4; v[5] = g5; v[6] = g6; v[7] = g7; v[8] = g8; v[9] = g9;
+          }
+          // lane L of the chunk's bit set takes the sums of chunk entry
+          // rank(L) from lane rank(L) * kBwdLanes
+          const uint32_t jr =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+          const int src = (int)(jr * (uint32_t)kBwdLanes) << 2;
+          const bool take = (cm >> lane) & 1ull;
+#pragma unroll
+          for (int q = 0; q < GS_PAIR_GRAD_FLOATS; ++q) {
+            const float t = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v[q])));
+            acc[q] += take ? t : 0.f;
+          }
+        };
+        auto run_word = [&](auto all_simple_tag) {
+          constexpr bool kAllSimple = decltype(all_simple_tag)::value;
+          unsigned long long m = mcell;
+          uint32_t kb = 0;
+          while (m) {
+            unsigned long long cm = 0;
+            int k = 0;
+            if (mine && rank - kb < (uint32_t)kBwdGroup) {
+              float4 *d = reinterpret_cast<float4 *>(&s_wrec[6 * (rank - kb)]);
+              d[0] = c0;
+              d[1] = c1;
+              d[2] = c2;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
+            const char *cb = reinterpret_cast<const char *>(s_wrec);
+#pragma unroll
+            for (int kk = 0; kk < kBwdGroup; ++kk) {
+              if (kk > 0 && !m) break;
+              const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+              m &= m - 1ull;
+              cm |= 1ull << bit;
+              const uint32_t ie = 64u * wd + bit;
+              const float4 r0v = reinterpret_cast<const float4 *>(cb + 48 * kk)[0];
+              const float4 r1v = reinterpret_cast<const float4 *>(cb + 48 * kk)[1];
+              const float2 pbz = reinterpret_cast<const float2 *>(cb + 48 * kk)[4];
+              const float dx = fx - r0v.x, dy = fy - r0v.y;
+              const float sq = conic_s(dx, dy, r0v.z, r1v.x, r0v.w);
+              const bool live = (ie < P.neval) && !(sq > kSkipS);
+              const float X = __builtin_fmaf(P.gR0, r1v.z,
+                                             __builtin_fmaf(P.gR1, r1v.w, __builtin_fmaf(P.gR2, pbz.x, P.gD * pbz.y)));
+              const bool simple = kAllSimple || ((simple_w >> bit) & 1ull);
+              float dop, cw;
+              if (simple) {
+                const float w = exp_neg_half(sq);
+                const float wv = live ? w : 0.f;
+                const float trans = P.T1;
+                const float c = trans * (r1v.y * wv);
+                P.A = P.A + c;
+                P.PG = __builtin_fmaf(c, X, P.PG);
+                P.T1 = 1.f - P.A;
+                const float inv = __builtin_amdgcn_rcpf(P.T1);
+                const float d_live = __builtin_fmaf(inv, P.PG, X);
+                const float dal = trans * (P.A >= kAlphaStop ? X + P.gA : d_live);
+                dop = dal * wv;
+                cw = c;
+              } else {
+                const float e = exp_inrange(-0.5f * sq);
+                const float w = sat01(e);
+                const float u = r1v.y * w;
+                const float ai = sat01(u);
+                const float trans = P.T1;
+                const float c = trans * (live ? ai : 0.f);
+                P.A = P.A + c;
+                P.PG = __builtin_fmaf(c, X, P.PG);
+                const bool term = P.A >= kAlphaStop;
+                P.T1 = 1.f - P.A;
+                const float inv = __builtin_amdgcn_rcpf(P.T1);
+                const float d_live = __builtin_fmaf(inv, P.PG, X);
+                const float dal = trans * (term ? X + P.gA : d_live);
+                const float g = (ai == u) ? dal * w : 0.f;
+                dop = (c > 0.f) ? g : 0.f;
+                cw = (w == e) ? c : -c;
+              }
+              s_dc[kk][lane] = make_float2(dop, cw);
+              k = kk + 1;
+            }
+            if (kAllSimple || (simple_w & cm) == cm) phase_b(std::false_type{}, cm, k); else phase_b(std::true_type{}, cm, k);
+            kb += (uint32_t)k;
+          }
+        };
+        if ((simple_w & mcell) == mcell) run_word(std::true_type{}); else run_word(std::false_type{});
+      }
+      // rotate: the next cell's state into cs[0] (a full cycle restores the order)
+      const BwdPixel t = cs[0];
+      const unsigned long long tm = mc[0];
+#pragma unroll
+      for (int q = 0; q + 1 < CPW; ++q) {
+        cs[q] = cs[q + 1];
+        mc[q] = mc[q + 1];
+      }
+      cs[CPW - 1] = t;
+      mc[CPW - 1] = tm;
+    }
+    // one partial per (entry, group): lanes of entries any of the cells replayed
+    if (mineU) {
+      const size_t sq = (size_t)slot * NG + (uint32_t)grp;
+      float *out = a.pair_grads + sq * GS_PARTIAL_STRIDE;
+      *reinterpret_cast<f4_u8 *>(out) = f4_u8{acc[0], acc[1], acc[2], acc[3]};
+      *reinterpret_cast<f4_u8 *>(out + 4) = f4_u8{acc[4], acc[5], acc[6], acc[7]};
+      *reinterpret_cast<f2_u8 *>(out + 8) = f2_u8{acc[8], acc[9]};
+      a.slot_live[sq] = 1;
+    }
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) mc[i] = mn[i];
+  }
+}
+
 // ======================================================== project bwd =====
-// Sum of each Gaussian's gradient partials: 8 lanes per Gaussian, lane
-// (h, q) walks g's slots h, h+2, h+4, ... of [pair_offset[g], pair_offset[g]
-// + touches) and adds the cell-q (q + 4, ...) partials slot_live flags (slot order),
-// then the 8 lane sums are added in a fixed DPP order -- bitwise
-// reproducible.  The four q lanes of a slot read its 160-B partial record
-// together, and consecutive Gaussians' slots are adjacent (index-order
-// slots): coalesced.  Flags of up to 4 slots are loaded at once, then their
-// partials: two round trips per 8 slots of g (the mean is 4.4 on C3).
-template <bool kT16>
-__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) {
+// Sum of each Gaussian's gradient partials: QL x HL lanes per Gaussian, lane
+// (h, q) walks g's slots h, h+HL, h+2HL, ... of [pair_offset[g],
+// pair_offset[g] + touches) and adds the partial groups q, q + QL, ... of
+// each (ng per slot: gs_partial_groups) that slot_live flags (slot order),
+// then the lane sums are added in a fixed DPP order -- bitwise reproducible.
+// The q lanes of a slot read its partial record together, and consecutive
+// Gaussians' slots are adjacent (index-order slots): coalesced.  Flags of up
+// to 4 slots are loaded at once, then their partials: two round trips per
+// 4 HL slots of g (the mean is 4.4 on C3).  Partials are 40 B, 8-B aligned:
+// read as float2.
+__device__ __forceinline__ float quad_sum(float v) {
+  v += dpp_row<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += dpp_row<0x4E>(v);  // quad_perm [2,3,0,1]
+  asm volatile("" : "+v"(v));
+  return v;
+}
+template <int LPG>
+__device__ __forceinline__ float lanes_sum(float v) {
+  if constexpr (LPG == 8) return oct_sum(v);
+  if constexpr (LPG == 4) return quad_sum(v);
+  if constexpr (LPG == 2) {
+    v += dpp_row<0xB1>(v);
+    asm volatile("" : "+v"(v));
+    return v;
+  }
+  return v;
+}
+
+#ifndef GS_GATHER_HL1
+#define GS_GATHER_HL1 4
+#endif
+constexpr int kGatherHL1 = GS_GATHER_HL1;  // slot lanes per Gaussian with one partial group per slot
+
+template <int QL, int HL>
+__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng) {
+  constexpr int LPG = QL * HL;
+  static_assert(LPG == 2 || LPG == 4 || LPG == 8, "lanes per Gaussian");
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const int g = (int)(t >> 3), h = (int)((t >> 2) & 1), q = (int)(t & 3);
+  const int g = (int)(t / LPG), h = (int)((t % LPG) / QL), q = (int)(t % QL);
   constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
   float2 acc[kF2];
 #pragma unroll
@@ -1567,40 +1924,38 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
   uint32_t off32 = a.pair_offset[gi];
   asm volatile("" : "+v"(off32));
   const uint32_t cnt = (valid && visb) ? rect_touches(tx0, tx1, ty0, ty1) : 0u;
-  // lane q sums cells q, q + 4, ... of the tile's Q (one pass when Q = 4)
-  const uint32_t ncell = (uint32_t)CellGeom(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size).cells();
-  for (uint32_t qc = (uint32_t)q; cnt > (uint32_t)h && qc < ncell; qc += 4) {
+  // lane q sums partial groups q, q + QL, ... of a slot's ng (one pass when ng <= QL)
+  for (uint32_t qc = (uint32_t)q; cnt > (uint32_t)h && qc < ng; qc += QL) {
     const size_t off = off32;
-    const uint8_t *flag = a.slot_live + off * ncell + qc;  // (slot e, cell qc) at flag[Q e]
-    // cell-qc partial of slot e at part + e * Q * GS_PARTIAL_STRIDE (dense 40-B
-    // records, 8-B aligned: global loads need 4-B alignment only)
-    const float *part = a.pair_grads + (off * ncell + qc) * GS_PARTIAL_STRIDE;
-    for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += 8) {
+    const uint8_t *flag = a.slot_live + off * ng + qc;  // (slot e, group qc) at flag[ng e]
+    // group-qc partial of slot e at part + e * ng * GS_PARTIAL_STRIDE (dense 40-B records)
+    const float2 *part = reinterpret_cast<const float2 *>(a.pair_grads + (off * ng + qc) * GS_PARTIAL_STRIDE);
+    for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += 4 * HL) {
       // the 4 flags in one round trip: unconditional loads (past the end
       // the clamped index re-reads slot e0), masked after
       uint32_t f[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const uint32_t e = e0 + 2 * i;
-        f[i] = flag[(size_t)ncell * (e < cnt ? e : e0)];
+        const uint32_t e = e0 + HL * i;
+        f[i] = flag[(size_t)ng * (e < cnt ? e : e0)];
       }
       // all four flags tested before any partial is requested: the partial
       // loads are conditional, so a wait for a later flag placed between them
       // would have to count them out conservatively and drain them
       uint32_t fm = 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fm |= (e0 + 2 * i < cnt && f[i]) ? 1u << i : 0u;
+      for (int i = 0; i < 4; ++i) fm |= (e0 + HL * i < cnt && f[i]) ? 1u << i : 0u;
       asm volatile("" : "+v"(fm));
 #pragma unroll
       for (int i = 0; i < 4; ++i) f[i] = (fm >> i) & 1u;
-      float4 va[4], vb[4];
-      float2 vc[4];
+      f4_u8 va[4], vb[4];
+      f2_u8 vc[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float4 *src = reinterpret_cast<const float4 *>(part + (size_t)(e0 + 2 * i) * ncell * GS_PARTIAL_STRIDE);
-        va[i] = f[i] ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
-        vb[i] = f[i] ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
-        vc[i] = f[i] ? *reinterpret_cast<const float2 *>(src + 2) : make_float2(0.f, 0.f);
+        const float *src = reinterpret_cast<const float *>(part + (size_t)(e0 + HL * i) * ng * kF2);
+        va[i] = f[i] ? *reinterpret_cast<const f4_u8 *>(src) : f4_u8{0.f, 0.f, 0.f, 0.f};
+        vb[i] = f[i] ? *reinterpret_cast<const f4_u8 *>(src + 4) : f4_u8{0.f, 0.f, 0.f, 0.f};
+        vc[i] = f[i] ? *reinterpret_cast<const f2_u8 *>(src + 8) : f2_u8{0.f, 0.f};
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1611,13 +1966,13 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a) 
       }
     }
   }
-  // ((q0 + q1) + (q2 + q3)) + (the other slot half's), on every lane of the 8
+  // the lane sums in a fixed DPP order, on every lane of the Gaussian's LPG
 #pragma unroll
   for (int k = 0; k < kF2; ++k) {
-    acc[k].x = oct_sum(acc[k].x);
-    acc[k].y = oct_sum(acc[k].y);
+    acc[k].x = lanes_sum<LPG>(acc[k].x);
+    acc[k].y = lanes_sum<LPG>(acc[k].y);
   }
-  if ((t & 7) == 0 && g < a.g.n) {
+  if ((t % LPG) == 0 && g < a.g.n) {
     float2 *out = reinterpret_cast<float2 *>(a.grad_sums) + (size_t)g * kF2;
 #pragma unroll
     for (int k = 0; k < kF2; ++k) out[k] = acc[k];
@@ -1937,6 +2292,12 @@ int cells_per_tile(int tile_size) {
   return qx * qx;
 }
 
+// gradient partials gs_blend_backward writes per list entry: the default
+// tile's waves combine kBwdCpw cells (k_blend_bwd_grp); other tiles one per cell
+int partial_groups(int tile_size) {
+  return tile_size == GS_DEFAULT_TILE ? 4 / kBwdCpw : cells_per_tile(tile_size);
+}
+
 // tile_size in range, image non-empty, tile coordinates fit 12 bits
 bool cam_ok(const gs_camera &c) {
   if (c.tile_size < 1 || c.tile_size > GS_MAX_TILE || c.image_width <= 0 || c.image_height <= 0) return false;
@@ -2115,6 +2476,10 @@ int32_t gs_tile_quads(int32_t tile_size) {
   return (tile_size < 1 || tile_size > GS_MAX_TILE) ? 0 : cells_per_tile(tile_size);
 }
 
+int32_t gs_partial_groups(int32_t tile_size) {
+  return (tile_size < 1 || tile_size > GS_MAX_TILE) ? 0 : partial_groups(tile_size);
+}
+
 size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles) {
   if (num_pairs < 0 || num_tiles < 0) return 0;
   return (size_t)num_pairs / 64u + (size_t)num_tiles + 2u;
@@ -2154,6 +2519,14 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (num_tiles <= 0) return GS_OK;
   const long long blocks = (long long)div_up(num_tiles, 8) * 8LL * cells_per_tile(a->cam.tile_size);
   if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_backward");
+  if constexpr (kBwdCpw > 1) {  // variant builds only (measured slower)
+    if (a->cam.tile_size == GS_DEFAULT_TILE) {
+      // (8 XCD bands of ceil(tiles / 8) tiles, partial_groups waves per tile)
+      k_blend_bwd_grp<kBwdCpw><<<(unsigned)(div_up(num_tiles, 8) * 8LL * partial_groups(GS_DEFAULT_TILE)), kWave,
+                                 0, s>>>(*a);
+      return check_launch("gs_blend_backward");
+    }
+  }
   if (a->cam.tile_size == GS_DEFAULT_TILE)
     k_blend_bwd<true><<<(unsigned)blocks, kWave, 0, s>>>(*a);
   else
@@ -2176,10 +2549,13 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   if (a->pair_grads && !cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
   if (a->pair_grads) {
-    if (a->cam.tile_size == GS_DEFAULT_TILE)
-      k_gather_slots<true><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
+    const uint32_t ng = (uint32_t)partial_groups(a->cam.tile_size);
+    if (ng == 1)
+      k_gather_slots<1, kGatherHL1><<<div_up((long long)kGatherHL1 * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
+    else if (ng == 2)
+      k_gather_slots<2, 2><<<div_up(4LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
     else
-      k_gather_slots<false><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a);
+      k_gather_slots<4, 2><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
   }
   const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
   if (hot)

@@ -57,6 +57,12 @@ class CameraParams:
         q = (self.tile_size + N.GS_QUAD - 1) // N.GS_QUAD
         return q * q
 
+    @property
+    def groups(self) -> int:
+        """Gradient partials the blend backward writes per list entry
+        (gs_partial_groups): 1 at the default tile, else one per cell."""
+        return _partial_groups(self.tile_size)
+
     def to_struct(self) -> N.GsCamera:
         c = N.GsCamera()
         c.image_width, c.image_height = int(self.image_width), int(self.image_height)
@@ -76,6 +82,16 @@ class CameraParams:
         R = ((v[0], v[1], v[2]), (v[4], v[5], v[6]), (v[8], v[9], v[10]))
         t = (v[3], v[7], v[11])
         return tuple(-(R[0][j] * t[0] + R[1][j] * t[1] + R[2][j] * t[2]) for j in range(3))
+
+
+_GROUPS: dict = {}
+
+
+def _partial_groups(tile_size: int) -> int:
+    g = _GROUPS.get(tile_size)
+    if g is None:
+        g = _GROUPS[tile_size] = int(N.load().gs_partial_groups(int(tile_size)))
+    return g
 
 
 def _rows(t: torch.Tensor, cols: int) -> Tuple[torch.Tensor, int]:
@@ -199,14 +215,15 @@ def window_holds(window, zmin_bits: int, zmax_bits: int) -> bool:
     return zmin_bits >= base and zmax_bits - base < _msd_limit(bits)
 
 
-def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cells: int, dev):
+def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cam: CameraParams, dev):
     """One byte buffer for T <= cap entries: tile keys + Gaussian ids
     (ping-pong, 16 B/entry), the tile sort's workspace, the liveness bitmap
-    (cells x gs_blend_live_words) and the backward's slot flags (cells B/entry)."""
+    (cells x gs_blend_live_words) and the backward's slot flags (partial
+    groups B/entry)."""
     nbytes = (16 * cap + 255) // 256 * 256
     nbytes += (int(lib.gs_radix_sort_workspace_bytes(cap)) + 255) // 256 * 256
-    nbytes += 8 * cells * int(lib.gs_blend_live_words(cap, num_tiles))
-    nbytes += (cells * cap + 255) // 256 * 256  # the backward's slot flags (zeroed by gs_tile_ranges)
+    nbytes += 8 * cam.cells * int(lib.gs_blend_live_words(cap, num_tiles))
+    nbytes += (cam.groups * cap + 255) // 256 * 256  # the backward's slot flags (zeroed by gs_tile_ranges)
     return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
 
 
@@ -312,7 +329,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         # drops entries past the capacity): its kernel time hides the
         # read-back's round trip.  T above the guess: re-allocate, re-emit.
         cap = _T_SEEN.get(dev, 0)
-        big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, cam.cells, dev) if cap else None
+        big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, cam, dev) if cap else None
         # (M, T) read back through pinned memory, copied BEFORE the emission
         # is queued, so the host wakes while the GPU still emits
         per_thread = getattr(_HOST_COUNTERS, "bufs", None)
@@ -366,7 +383,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     # queued.
     emitted = big_guess is not None and big_guess[1] >= T
     if not emitted:
-        layout = _tile_layout(lib, _alloc_tile_buffers(lib, T, num_tiles, cam.cells, dev), num_tiles, cam)
+        layout = _tile_layout(lib, _alloc_tile_buffers(lib, T, num_tiles, cam, dev), num_tiles, cam)
         ba.tile_keys, ba.pair_gauss, ba.capacity = layout.p_tk[0], layout.p_tv[0], layout.cap
         StageTimer.mark("bin_emit")
         N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
@@ -377,7 +394,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
                                     L.p_ws, L.ws_bytes, C.byref(alt), s), "tile sort")
     # (with gradients to come: the backward's slot flags zeroed in the same kernel)
     ra = N.GsRangeArgs(T, num_tiles, L.p_tk[alt.value], N.ptr(ranges),
-                       L.big.data_ptr() + L.o_flags if need_grad else None, cam.cells)
+                       L.big.data_ptr() + L.o_flags if need_grad else None, cam.groups)
     StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
@@ -396,7 +413,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     fr.live_bits = L.big[L.o_live:L.o_live + 8 * cam.cells * L.live_words].view(torch.int64).view(cam.cells,
                                                                                                L.live_words)
     fr.big = L.big
-    fr.slot_live = L.big[L.o_flags:L.o_flags + cam.cells * T] if need_grad else None
+    fr.slot_live = L.big[L.o_flags:L.o_flags + cam.groups * T] if need_grad else None
     fr.pair_offset, fr.ranges = pair_offset, ranges
     fr.pix_acc, fr.pix_state = pix_acc, pix_state
     return image, alpha, depth, means2d, conics, radii, vis, fr
@@ -425,12 +442,12 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_image = g_image.contiguous()
         g_alpha = None if g_alpha is None else g_alpha.contiguous()
         g_depth = None if g_depth is None else g_depth.contiguous()
-        # one partial per (slot, 8x8 cell of the tile); only the cells that
-        # replay an entry write theirs and set its flag
-        pair_grads = torch.empty((fr.T * cam.cells, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
+        # one partial per (slot, partial group of the tile: gs_partial_groups);
+        # only the groups that replay an entry write theirs and set its flag
+        pair_grads = torch.empty((fr.T * cam.groups, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
         slot_live = fr.slot_live  # (zeroed by the forward's gs_tile_ranges)
         if slot_live is None:
-            slot_live = torch.zeros((fr.T * cam.cells,), dtype=torch.uint8, device=dev)
+            slot_live = torch.zeros((fr.T * cam.groups,), dtype=torch.uint8, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
