@@ -185,9 +185,11 @@ def main():
                 p.grad = None
         out = renderer.render(cam, model, settings)
         torch.autograd.backward([out["image"], out["alpha"], out["depth"]], cot)
-        if reducer is not None:
+        if reducer is not None and opt is not None:
+            reducer.reduce_and_step(opt)  # (pipelined per range when the backward handed over ranges)
+        elif reducer is not None:
             reducer.all_reduce_mean()
-        if opt is not None:
+        elif opt is not None:
             opt.step()
         frames.append(out)
 

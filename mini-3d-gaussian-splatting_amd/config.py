@@ -50,6 +50,9 @@ class TrainingConfig:
     seed: int = 0
     sh_degree: int = 0                 # max SH degree of the colour (0 = the reference's DC-only render)
     sh_increase_interval: int = 1000   # active SH degree +1 every this many iterations, up to sh_degree
+    # after a densification the reference builds a fresh Adam (optimizer.py:133-137: moments and step
+    # counts dropped); False keeps the kept Gaussians' moments (new ones start at zero)
+    reset_adam_on_densify: bool = False
 
 
 def _need_yaml():

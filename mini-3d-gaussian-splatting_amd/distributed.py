@@ -98,7 +98,7 @@ class GradAllReduce:
         op = self.dist.ReduceOp.AVG if self._avg else self.dist.ReduceOp.SUM
         self.ranges_reduced += 1
         if lo == 0 and hi == n:  # every row: the whole bucket in one call
-            self._works.append(self.dist.all_reduce(flat, op=op, group=self.group, async_op=True))
+            self._works.append((lo, hi, [self.dist.all_reduce(flat, op=op, group=self.group, async_op=True)]))
             return
         # the range's slice of every parameter, coalesced into one collective
         # (one RCCL group launch) where the backend supports it
@@ -112,10 +112,16 @@ class GradAllReduce:
             with cm_fn(group=self.group, device=flat.device, async_ops=True) as cm:
                 for t in slices:
                     self.dist.all_reduce(t, op=op, group=self.group)
-            self._works.append(cm)
+            self._works.append((lo, hi, [cm]))
             return
-        for t in slices:
-            self._works.append(self.dist.all_reduce(t, op=op, group=self.group, async_op=True))
+        self._works.append((lo, hi, [self.dist.all_reduce(t, op=op, group=self.group, async_op=True)
+                                     for t in slices]))
+
+    def covers(self, leaves) -> bool:
+        """Do `leaves` write every parameter of the bucket?  Only then may the
+        backward hand rows to rows_ready (a parameter no kernel writes would
+        be reduced from uninitialised bucket memory)."""
+        return {id(t) for t in leaves} == {id(p) for p in self.params}
 
     def grad_destinations(self, leaves) -> Optional[List[torch.Tensor]]:
         """Bucket views shaped like `leaves`, when every leaf is one of this
@@ -139,8 +145,9 @@ class GradAllReduce:
         in_place = [self._aliases(p, v) for p, v in zip(self.params, views)]
         if self._works:
             # the backward reduced the bucket range by range (rows_ready)
-            for w in self._works:
-                w.wait()
+            for _, _, ws in self._works:
+                for w in ws:
+                    w.wait()
             self._works = []
             if not self._avg:
                 flat.div_(self.dist.get_world_size(self.group))
@@ -155,11 +162,44 @@ class GradAllReduce:
         world = self.dist.get_world_size(self.group)
         if self._avg:
             # RCCL divides inside the reduction: no extra pass over the bucket
-            self.dist.all_reduce(flat, op=self.dist.ReduceOp.AVG, group=self.group)
-        else:
+            try:
+                self.dist.all_reduce(flat, op=self.dist.ReduceOp.AVG, group=self.group)
+            except RuntimeError:
+                # a backend that has the enum but rejects AVG at run time: SUM and
+                # one division from now on (the failed call reduced nothing)
+                self._avg = False
+        if not self._avg:
             self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
             flat.div_(world)
         self._copy_out(views, in_place)
+
+    def reduce_and_step(self, optimizer) -> None:
+        """all_reduce_mean() then optimizer.step(), pipelined when the
+        backward handed its rows over in ranges (rows_ready) and every
+        gradient is the bucket itself: range k's Adam update is queued behind
+        range k's all-reduce only (FusedAdam.step_ranges), so it overlaps the
+        reductions of the later ranges.  Bit-identical to the unpipelined
+        sequence (the same reduced values, an elementwise update)."""
+        flat = self._bucket()
+        views = torch.split(flat, self._sizes)
+        pipelined = (len(self._works) > 1 and hasattr(optimizer, "step_ranges")
+                     and all(self._aliases(p, v) for p, v in zip(self.params, views)))
+        if not pipelined:
+            self.all_reduce_mean()
+            optimizer.step()
+            return
+        works, self._works = self._works, []
+        n = self.params[0].shape[0]
+        world = self.dist.get_world_size(self.group)
+
+        def before(k):
+            lo, hi, ws = works[k]
+            for w in ws:
+                w.wait()  # (RCCL: the current stream waits for this range's collective)
+            if not self._avg:
+                for v in views:
+                    v.view(n, -1)[lo:hi].div_(world)
+        optimizer.step_ranges([(lo, hi) for lo, hi, _ in works], before)
 
     def _copy_out(self, views, in_place) -> None:
         for p, v, ok in zip(self.params, views, in_place):

@@ -20,12 +20,10 @@ class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
 
-    @torch.no_grad()
-    def step(self, closure=None):
-        loss = None
-        if closure is not None:
-            with torch.enable_grad():
-                loss = closure()
+    def _begin(self):
+        """Advance every parameter with a gradient by one step: the descriptors
+        (param, moments, grad, row count, lr, bias corrections) of this step,
+        grouped by (beta1, beta2, eps)."""
         batches = {}
         for group in self.param_groups:
             b1, b2 = group["betas"]
@@ -41,9 +39,16 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] += 1
                 t = st["step"]
-                d = N.GsAdamTensor(N.ptr(p), N.ptr(st["exp_avg"]), N.ptr(st["exp_avg_sq"]), N.ptr(p.grad),
-                                   p.numel(), float(group["lr"]), 1.0 - b1 ** t, (1.0 - b2 ** t) ** 0.5)
-                batches.setdefault((float(b1), float(b2), float(group["eps"])), []).append(d)
+                rows = p.shape[0] if p.dim() else 1
+                batches.setdefault((float(b1), float(b2), float(group["eps"])), []).append(
+                    (p, st["exp_avg"], st["exp_avg_sq"], p.grad, rows, float(group["lr"]), 1.0 - b1 ** t,
+                     (1.0 - b2 ** t) ** 0.5))
+        return batches
+
+    @staticmethod
+    def _launch(batches, lo=None, hi=None):
+        """One gs_adam_step per (betas, eps) batch of <= 8 tensors, over rows
+        [lo, hi) of each (dim 0; all rows when lo is None)."""
         lib = N.load()
         stream = torch.cuda.current_stream().cuda_stream
         for (b1, b2, eps), ds in batches.items():
@@ -51,10 +56,38 @@ class FusedAdam(torch.optim.Optimizer):
                 chunk = ds[i:i + N.GS_ADAM_MAX_TENSORS]
                 a = N.GsAdamArgs()
                 a.num_tensors, a.beta1, a.beta2, a.eps = len(chunk), b1, b2, eps
-                for k, d in enumerate(chunk):
-                    a.t[k] = d
+                for k, (p, m, v, g, rows, lr, bc1, bc2s) in enumerate(chunk):
+                    if lo is None:
+                        off, num = 0, p.numel()
+                    else:
+                        cols = p.numel() // max(rows, 1)
+                        r0, r1 = min(lo, rows), min(hi, rows)
+                        off, num = r0 * cols, (r1 - r0) * cols
+                    a.t[k] = N.GsAdamTensor(N.ptr(p) + 4 * off, N.ptr(m) + 4 * off, N.ptr(v) + 4 * off,
+                                            N.ptr(g) + 4 * off, num, lr, bc1, bc2s)
                 N.check(lib.gs_adam_step(C.byref(a), stream), "gs_adam_step")
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._launch(self._begin())
         return loss
+
+    @torch.no_grad()
+    def step_ranges(self, ranges, before=None):
+        """The same update as step() (Adam is elementwise: bit-identical),
+        launched over row ranges [lo, hi) of every parameter in turn; before(k),
+        when given, runs before range k is queued -- the data-parallel
+        reducer makes the stream wait for range k's all-reduce there, so
+        range k's update overlaps the reductions of the ranges after it."""
+        batches = self._begin()
+        for k, (lo, hi) in enumerate(ranges):
+            if before is not None:
+                before(k)
+            self._launch(batches, lo, hi)
 
 
 # --------------------------------------------------------------------------
@@ -103,8 +136,10 @@ class DensityController:
 
 class GaussianOptimizer:
     """optimizer.py:90-141 with FusedAdam over the reference's five groups.
-    After densification the Adam moments are remapped (the reference's
-    setup_optimizer() would drop them, optimizer.py:133-137)."""
+    After densification the Adam moments are remapped, kept Gaussians
+    carrying theirs; with config.reset_adam_on_densify a fresh optimizer is
+    built instead, as the reference's setup_optimizer() does
+    (optimizer.py:133-137: every moment and step count dropped)."""
 
     def __init__(self, gaussians, config):
         self.gaussians, self.config = gaussians, config
@@ -141,7 +176,10 @@ class GaussianOptimizer:
 
     def densify_and_prune(self, iteration: int, scene_extent: float):
         if self.density_controller.should_densify(iteration):
-            return self.density_controller.densify_and_prune(self.gaussians, self.optimizer, iteration, scene_extent)
+            info = self.density_controller.densify_and_prune(self.gaussians, self.optimizer, iteration, scene_extent)
+            if getattr(self.config, "reset_adam_on_densify", False):
+                self.setup_optimizer()
+            return info
         return None
 
     def reset_opacity(self) -> None:

@@ -172,7 +172,19 @@ _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess
 # two per-device guesses above are only guesses, a stale one is corrected)
 _HOST_COUNTERS = threading.local()
 _FUSE_FLAGS = os.environ.get("GS_FUSE_SLOT_FLAGS", "1") != "0"  # slot flags zeroed by gs_tile_ranges
-_DEPTH_WINDOW: dict = {}  # device -> (key_base, key_bits) from its last frame's visible depth range
+# Depth-key windows (per process and device; these are guesses, a stale one
+# only costs a re-render, so host threads may race on them): the window
+# covers the union of the last _WINDOW_FRAMES frames' visible depth ranges, so
+# views that alternate (a trainer's shuffled cameras) keep fitting it.  A
+# frame whose depths leave the window (a miss) is rendered again with 32-bit
+# keys; a second miss within _MISS_SPAN frames turns windows off for
+# _WINDOW_OFF_FRAMES frames (a miss costs a whole re-render, a window saves
+# ~20 us of sorting).
+_DEPTH_HIST: dict = {}  # device -> [(zmin_bits, zmax_bits)] of its last frames
+_WINDOW_FRAMES = 8
+_MISS_SPAN = 32
+_WINDOW_OFF_FRAMES = 256
+_WINDOW_STATE: dict = {}  # device -> {"frame", "misses", "last_miss", "off_until"}
 # Windowed depth keys of 9..31 bits are sorted by gs_depth_sort_msd (one MSD pass + a sort per
 # bucket in LDS) unless GS_DEPTH_MSD=0.  A bucket over its LDS capacity (clumped depths) poisons
 # the frame's depth max (0xFFFFFFFF): the frame is sorted again with the LSD passes, and the LSD
@@ -205,6 +217,49 @@ def _msd_limit(bits: int) -> int:
     culled sentinel) and, from 9 bits on, 255 << (bits - 8), so that the top
     digit of gs_depth_sort_msd's MSD pass holds the sentinel only."""
     return min((1 << bits) - 1, 255 << (bits - 8)) if bits >= 9 else (1 << bits) - 1
+
+
+def _window_state(dev) -> dict:
+    st = _WINDOW_STATE.get(dev)
+    if st is None:
+        st = _WINDOW_STATE[dev] = {"frame": 0, "misses": 0, "last_miss": None, "off_until": 0}
+    return st
+
+
+def _window_for(dev):
+    """The depth-key window of this device's next frame (None: 32-bit keys)."""
+    st = _window_state(dev)
+    hist = _DEPTH_HIST.get(dev)
+    if not hist or st["frame"] < st["off_until"]:
+        return None
+    return depth_window(min(h[0] for h in hist), max(h[1] for h in hist))
+
+
+def _record_depths(dev, zmin_bits: int, zmax_bits: int) -> None:
+    """A finished frame's visible depth-bit range (none visible: nothing)."""
+    st = _window_state(dev)
+    st["frame"] += 1
+    if zmin_bits > zmax_bits:
+        return
+    hist = _DEPTH_HIST.setdefault(dev, [])
+    hist.append((zmin_bits, zmax_bits))
+    del hist[:-_WINDOW_FRAMES]
+
+
+def _note_window_miss(dev) -> None:
+    st = _window_state(dev)
+    st["misses"] += 1
+    if st["last_miss"] is not None and st["frame"] - st["last_miss"] <= _MISS_SPAN:
+        st["off_until"] = st["frame"] + _WINDOW_OFF_FRAMES
+    st["last_miss"] = st["frame"]
+
+
+def depth_window_stats(dev=None) -> dict:
+    """Frames rendered and window misses (re-renders) per device: a
+    measurement of the depth-key window's hit rate."""
+    if dev is not None:
+        return dict(_window_state(torch.device(dev)))
+    return {str(d): dict(v) for d, v in _WINDOW_STATE.items()}
 
 
 def window_holds(window, zmin_bits: int, zmax_bits: int) -> bool:
@@ -281,7 +336,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     vals = torch.empty((2, n), dtype=i32, device=dev)
     counters = torch.empty((N.GS_NUM_COUNTERS,), dtype=i32, device=dev)
     key_minmax = torch.empty((2 * max(1, (n + 255) // 256),), dtype=i32, device=dev)
-    window = _DEPTH_WINDOW.get(dev) if depth_window_ok else None
+    window = _window_for(dev) if depth_window_ok else None
     key_base, key_bits = window if window is not None else (0, 32)
 
     StageTimer.mark("project_fwd")
@@ -296,10 +351,13 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         ws = torch.empty((lib.gs_radix_sort_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         StageTimer.mark("depth_sort")
         alt = C.c_int32(0)
+        # (the MSD backoff counts only frames that would have taken the MSD
+        # sort; it is per process and device, not per host thread)
+        msd = _DEPTH_MSD and window is not None and 9 <= key_bits <= 31
         backoff = _MSD_BACKOFF.get(dev, 0)
-        if backoff:
+        if msd and backoff:
             _MSD_BACKOFF[dev] = backoff - 1
-        if _DEPTH_MSD and window is not None and 9 <= key_bits <= 31 and not backoff:
+        if msd and not backoff:
             N.check(lib.gs_depth_sort_msd(N.ptr(keys[0]), N.ptr(vals[0]), N.ptr(keys[1]), N.ptr(vals[1]), n,
                                           key_bits, N.ptr(ws), ws.numel(), N.ptr(key_minmax) + 4, C.byref(alt),
                                           s), "depth sort (msd)")
@@ -357,8 +415,9 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
             # or an MSD bucket over capacity (the depth max poisoned)
             if zmax == _POISON:
                 _MSD_BACKOFF[dev] = _MSD_BACKOFF_FRAMES
+            else:
+                _note_window_miss(dev)
             _T_SEEN[dev] = T
-            _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
             return forward_pipeline(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit,
                                     sh_rest, sh_degree, pair_counts, depth_window_ok=False, need_grad=need_grad)
     else:
@@ -368,7 +427,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     if M == 0:
         if n > 0:
             _T_SEEN[dev] = T
-            _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
+            _record_depths(dev, zmin, zmax)
         # renderer.py:74-83: bg once (not doubled, not clamped), zero alpha/depth
         bg = torch.tensor(cam.bg, dtype=f32, device=dev).view(3, 1, 1)
         image = bg.repeat(1, H, W)
@@ -405,7 +464,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
     StageTimer.mark("~end_fwd")
     _T_SEEN[dev] = T  # (the next frame's guesses: after the launches)
-    _DEPTH_WINDOW[dev] = depth_window(zmin, zmax)
+    _record_depths(dev, zmin, zmax)
 
     # (the blend is queued: views for the frame cost no GPU idle time now)
     kv = L.big[:16 * L.cap].view(i32).view(4, L.cap)

@@ -129,7 +129,12 @@ class GaussianRenderer:
                 if views is None:
                     return None
                 d = dict(zip(names, views))
-                if hasattr(sink, "rows_ready"):  # reduce finished ranges during the backward
+                # reduce finished ranges during the backward -- only when the
+                # render writes every row of the bucket: a bucket parameter the
+                # render does not reach (e.g. _features_rest with sh_degree 0
+                # while the model's active degree is > 0) is filled (zero or
+                # its .grad) by all_reduce_mean before its collective instead
+                if hasattr(sink, "rows_ready") and getattr(sink, "covers", lambda _: False)(leaves):
                     d["_rows_ready"], d["_chunks"] = sink.rows_ready, sink.overlap_chunks()
                 return d
         image, alpha, depth, means2d, conics, radii, vis = rasterize(

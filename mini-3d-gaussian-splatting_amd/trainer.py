@@ -116,10 +116,13 @@ class GaussianTrainer:
         target = camera._image
         total, l1, dssim = photometric_loss(out["image"], target, self.config.lambda_dssim)
         total.backward()
-        if self._dist is not None:
-            self._reducer.all_reduce_mean()
         opt.update_learning_rate(self.iteration)
-        opt.step()
+        if self._dist is not None:
+            # mean all-reduce, then Adam; pipelined per Gaussian range when the
+            # backward handed its rows over in ranges (GS_ALLREDUCE_CHUNKS)
+            self._reducer.reduce_and_step(opt.optimizer)
+        else:
+            opt.step()
         info = opt.densify_and_prune(self.iteration, self.scene_extent)
         if info is not None:
             self._reducer = None

@@ -10,9 +10,12 @@ Tolerances (north_star: outputs within 1e-4 fp32 of the reference):
     came within a few ulps of a decision threshold (knife_edge below; the
     GPU's exp is ~1 ulp from glibc's, so such a pixel may decide the
     other way), each one reported
-  * gradients: |d - d_ref| <= 2e-3 * max|d_ref| + 1e-5 per tensor
+  * gradients: |d - d_ref| <= 1e-4 * max|d_ref| + 1e-7 per tensor
     (reference backward is autograd over a different but algebraically
-    identical expression order)
+    identical expression order).  On oracle scenes
+    with knife-edge pixels that flipped, the Gaussians whose footprint
+    covers such a pixel (touching_gaussians) are exempt and reported: a
+    flipped termination changes every contributor's dL/dalpha there.
 """
 from __future__ import annotations
 
@@ -26,8 +29,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 IMG_ATOL = 1e-4
-GRAD_RTOL = 2e-3
-GRAD_ATOL = 1e-5
+GRAD_RTOL = 1e-4
+GRAD_ATOL = 1e-7
 
 
 def oracle():
@@ -125,12 +128,40 @@ def check_projection(out, ref, atol=IMG_ATOL):
     return errs
 
 
-def check_grad(name, d, dref, rtol=GRAD_RTOL, atol=GRAD_ATOL):
+def check_grad(name, d, dref, rtol=GRAD_RTOL, atol=GRAD_ATOL, rows=None):
+    """rows: optional [N] bool, the Gaussians to check (the scale stays the
+    whole tensor's max |d_ref|)."""
     d = np.asarray(d, np.float64).reshape(np.shape(dref))
     dref = np.asarray(dref, np.float64)
     scale = float(np.max(np.abs(dref))) if dref.size else 0.0
+    if rows is not None:
+        d, dref = d[rows], dref[rows]
     e = max_err(d, dref)
     tol = rtol * scale + atol
+    print(f"  grad {name}: max err {e / max(scale, 1e-30):.3g} of scale {scale:.3g}")
     if not e <= tol:
         return [f"grad {name}: max abs err {e:.3g} > tol {tol:.3g} (scale {scale:.3g})"]
     return []
+
+
+def grad_rel_err(d, dref, rows=None):
+    """max |d - d_ref| over `rows` / max |d_ref| over all rows."""
+    d = np.asarray(d, np.float64).reshape(np.shape(dref))
+    dref = np.asarray(dref, np.float64)
+    scale = max(float(np.max(np.abs(dref))) if dref.size else 0.0, 1e-30)
+    if rows is not None:
+        d, dref = d[rows], dref[rows]
+    return max_err(d, dref) / scale
+
+
+def touching_gaussians(means2d, conics, vis, pixels, s_max=23.1 * 1.01):
+    """[N] bool: visible Gaussians whose blend footprint (s = d^T Q d <=
+    s_max, the :336 skip with a 1 % margin) covers any of `pixels` [(y, x)]."""
+    mu = np.asarray(means2d, np.float64)
+    q = np.asarray(conics, np.float64).reshape(-1, 4)
+    hit = np.zeros(len(mu), bool)
+    for y, x in pixels:
+        dx, dy = x - mu[:, 0], y - mu[:, 1]
+        s = dx * dx * q[:, 0] + dx * dy * (q[:, 1] + q[:, 2]) + dy * dy * q[:, 3]
+        hit |= ~(s > s_max)  # (NaN counts as touching)
+    return hit & np.asarray(vis, bool)

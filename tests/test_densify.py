@@ -28,7 +28,10 @@ def normal_of(seed, i, k):
     return math.sqrt(-2.0 * math.log(u1)) * math.cos(2 * math.pi * u2)
 
 
-def ref_densify(m, grad, th, extent, min_op, seed):
+def ref_densify(m, grad, th, extent, min_op, seed, masks=False):
+    """The statement; masks=True also returns (keep, split, clone, hot, s, o)
+    over the input Gaussians (the trainer parity test remaps Adam moments
+    with them and checks no decision sits on a threshold)."""
     xyz, fdc, frest, scl, rot, op = [p.detach().cpu().double() for p in m.parameter_list()]
     g = grad.detach().cpu().double()
     n = xyz.shape[0]
@@ -53,7 +56,10 @@ def ref_densify(m, grad, th, extent, min_op, seed):
         "rot": [rot[keep], q[sp], q[sp], rot[cl]],
         "op": [op[keep], child_op[sp, None], child_op[sp, None], op[cl]],
     }
-    return {k: torch.cat(v) for k, v in rows.items()}, (int(keep.sum()), int(sp.sum()), int(cl.sum()))
+    out = {k: torch.cat(v) for k, v in rows.items()}, (int(keep.sum()), int(sp.sum()), int(cl.sum()))
+    if masks:
+        return out + ((keep, sp, cl, hot, s, o),)
+    return out
 
 
 def _model(pkg, cuda, n=6000, seed=4):

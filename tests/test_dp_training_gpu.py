@@ -54,15 +54,19 @@ def _mean_of_views_reference(pkg, ds, cfg, world):
     return tr
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_dp_trainer_two_ranks_match_mean_of_views(pkg, cuda, tmp_path, overlap):
-    """overlap: the render backward hands its gradient rows to the all-reduce
-    in two ranges (GradAllReduce.rows_ready), the first reduced while the
-    second is computed; without: one reduction after the backward."""
+@pytest.mark.parametrize("chunks", [1, 2, 4])
+def test_dp_trainer_two_ranks_match_mean_of_views(pkg, cuda, tmp_path, chunks):
+    """chunks > 1: the render backward hands its gradient rows to the
+    all-reduce in that many ranges (GradAllReduce.rows_ready), range k
+    reduced while range k+1 is computed, and FusedAdam updates range k as
+    soon as its reduction is done (GradAllReduce.reduce_and_step ->
+    FusedAdam.step_ranges); chunks = 1: one reduction after the backward,
+    then one Adam launch.  Every setting must equal the single-process
+    mean-of-views step bit for bit, densification included."""
     write_scene_files(tmp_path)
     port = _free_port()
     outs = [tmp_path / f"rank{r}.npz" for r in range(2)]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", GS_ALLREDUCE_CHUNKS="2" if overlap else "1",
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", GS_ALLREDUCE_CHUNKS=str(chunks),
                GS_ALLREDUCE_MIN_ROWS="256")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), str(r), "2", str(port),
                                str(tmp_path), str(outs[r])], env=env) for r in range(2)]
@@ -76,7 +80,7 @@ def test_dp_trainer_two_ranks_match_mean_of_views(pkg, cuda, tmp_path, overlap):
     a, b = (np.load(o) for o in outs)
     assert int(a["iteration"]) == 3 and int(a["n"]) == int(b["n"])
     # iteration 3's reducer (rebuilt after the densification): ranges it reduced
-    assert int(a["ranges"]) == (2 if overlap else 1)
+    assert int(a["ranges"]) == chunks
     for i in range(6):
         assert np.array_equal(a[f"p{i}"], b[f"p{i}"]), f"replicas diverged in parameter {i}"
     ds = load_scene(pkg, tmp_path, cuda, split=False)

@@ -468,14 +468,23 @@ def _scene_vs_oracle(pkg, cuda, sc, W, H, bg, seed=1, renderer_kw=None, knife=Tr
     errs = G.check_image(o, ref, exempt=edge if knife else None) + G.check_projection(o, ref)
     ds, dr = G.oracle().covariance_backward(sc.scaling.numpy(), sc.rotation.numpy(), ref["grads"]["cov3d"])
     op = torch.sigmoid(sc.opacity[:, 0]).numpy()
-    for name, d, r in (("xyz", _np(m._xyz.grad), ref["grads"]["xyz"]), ("scaling", _np(m._scaling.grad), ds),
-                       ("rotation", _np(m._rotation.grad), dr)):
-        print(f"{label} grad {name}: max err / max|ref| = {G.max_err(d, r) / max(np.abs(r).max(), 1e-30):.3g}")
-    errs += G.check_grad("xyz", _np(m._xyz.grad), ref["grads"]["xyz"])
-    errs += G.check_grad("scaling", _np(m._scaling.grad), ds)
-    errs += G.check_grad("rotation", _np(m._rotation.grad), dr)
-    errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"])
-    errs += G.check_grad("opacity", _np(m._opacity.grad)[:, 0], ref["grads"]["opacity"] * op * (1 - op))
+    # Gradients: a flipped knife-edge pixel changes the gradient of every
+    # Gaussian in its chain; those Gaussians (footprint covering the pixel)
+    # are exempt from the 1e-4 check and reported beside the others
+    flipped = list(zip(*np.nonzero(bad & edge))) if knife else []
+    touch = G.touching_gaussians(o["means2d"], o["conics"], o["vis"], flipped)
+    rows = ~touch
+    pairs = (("xyz", _np(m._xyz.grad), ref["grads"]["xyz"]), ("scaling", _np(m._scaling.grad), ds),
+             ("rotation", _np(m._rotation.grad), dr),
+             ("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"]),
+             ("opacity", _np(m._opacity.grad)[:, 0], ref["grads"]["opacity"] * op * (1 - op)))
+    for name, d, r in pairs:
+        msg = f"{label} grad {name}: max err / max|ref| = {G.grad_rel_err(d, r, rows):.3g} over the {int(rows.sum())}"
+        msg += f" Gaussians off the flipped pixels"
+        if touch.any():
+            msg += f"; {G.grad_rel_err(d, r, touch):.3g} over the {int(touch.sum())} touching them"
+        print(msg)
+        errs += G.check_grad(name, d, r, rows=rows)
     return errs, bad, edge
 
 
@@ -665,10 +674,12 @@ def test_rccl_range_reduction_world1(pkg, cuda):
 
 
 def test_depth_window_miss_rerenders(pkg, cuda):
-    """The depth sort runs over a window of key bits chosen from the previous
-    frame's visible depth range (rasterizer.depth_window); a frame whose depths
-    leave the window is rendered again with 32-bit keys.  Both a held window
-    and a missed one give the frame a fresh renderer gives, bit for bit."""
+    """The depth sort runs over a window of key bits chosen from the union of
+    the last frames' visible depth ranges (rasterizer._window_for); a frame
+    whose depths leave the window is rendered again with 32-bit keys (a miss,
+    counted), and a second miss within _MISS_SPAN frames turns windows off for
+    a while.  Held, missed and windowless frames all equal the frame a fresh
+    renderer gives, bit for bit."""
     RZ = pkg.rasterizer
     syn = pkg.synthetic
     W, H = 320, 240
@@ -681,23 +692,44 @@ def test_depth_window_miss_rerenders(pkg, cuda):
         (out["image"].sum() + out["depth"].sum()).backward()
         return out["image"].clone(), out["depth"].clone(), m._xyz.grad.clone(), m._scaling.grad.clone()
 
-    RZ._DEPTH_WINDOW.pop(cuda, None)
-    fresh_wide = frame(wide)             # 32-bit keys (no window yet)
-    frame(narrow)                        # leaves a narrow window behind
-    assert RZ._DEPTH_WINDOW[cuda] is not None and RZ._DEPTH_WINDOW[cuda][1] <= 24
-    missed = frame(wide)                 # leaves the window: re-rendered with 32-bit keys
-    held = frame(wide)                   # its own window now
-    assert RZ._DEPTH_WINDOW[cuda] is None or RZ._DEPTH_WINDOW[cuda][1] > 16
-    frame(narrow)
-    held_narrow = frame(narrow)
-    RZ._DEPTH_WINDOW.pop(cuda, None)
-    fresh_narrow = frame(narrow)
-    for a, b in zip(fresh_wide, missed):
-        assert torch.equal(a, b)
-    for a, b in zip(fresh_wide, held):
-        assert torch.equal(a, b)
-    for a, b in zip(fresh_narrow, held_narrow):
-        assert torch.equal(a, b)
+    def reset():
+        RZ._DEPTH_HIST.pop(cuda, None)
+        RZ._WINDOW_STATE.pop(cuda, None)
+
+    def misses():
+        return RZ.depth_window_stats(cuda)["misses"]
+
+    try:
+        reset()
+        fresh_wide = frame(wide)             # 32-bit keys (no history yet)
+        reset()
+        frame(narrow)                        # a narrow window for the next frame
+        w = RZ._window_for(cuda)
+        assert w is not None and w[1] <= 24
+        missed = frame(wide)                 # leaves the window: re-rendered with 32-bit keys
+        assert misses() == 1
+        held = frame(wide)                   # the union of both ranges now
+        frame(narrow)
+        held_narrow = frame(narrow)          # inside the union: no miss
+        assert misses() == 1
+        reset()
+        fresh_narrow = frame(narrow)
+        for a, b in zip(fresh_wide, missed):
+            assert torch.equal(a, b)
+        for a, b in zip(fresh_wide, held):
+            assert torch.equal(a, b)
+        for a, b in zip(fresh_narrow, held_narrow):
+            assert torch.equal(a, b)
+        # once the wide frame has left the history, it misses again; a second
+        # miss within _MISS_SPAN frames switches the windows off
+        for _ in range(RZ._WINDOW_FRAMES):
+            frame(narrow)
+        again = frame(wide)
+        assert misses() == 2 and RZ._window_for(cuda) is None
+        for a, b in zip(fresh_wide, again):
+            assert torch.equal(a, b)
+    finally:
+        reset()
 
 
 def test_no_gaussians(pkg, cuda):

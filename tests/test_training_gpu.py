@@ -28,9 +28,17 @@ def test_trainer_learns_and_checkpoints(pkg, cuda, tmp_path):
     tr.setup()
     before = tr.validate()
     n0 = tr.gaussians.get_num_points()
+    RZ = pkg.rasterizer
+    RZ._WINDOW_STATE.pop(cuda, None)
+    RZ._DEPTH_HIST.pop(cuda, None)
     tr.train()
+    # the depth-key window under shuffled training cameras: a miss re-renders a
+    # frame, so the hit rate has to stay high (advisor, round 2)
+    ws = RZ.depth_window_stats(cuda)
     after = tr.validate()
-    print(f"PSNR {before['psnr']:.2f} -> {after['psnr']:.2f} dB; Gaussians {n0} -> {after['num_gaussians']}")
+    print(f"PSNR {before['psnr']:.2f} -> {after['psnr']:.2f} dB; Gaussians {n0} -> {after['num_gaussians']}; "
+          f"depth-window misses {ws['misses']} in {ws['frame']} frames")
+    assert ws["frame"] >= cfg.iterations and ws["misses"] <= 0.02 * ws["frame"]
     assert after["psnr"] > before["psnr"] + 5.0
     assert after["num_gaussians"] != n0  # density control ran
     assert len(tr.train_losses) == 6 and tr.train_losses[-1] < tr.train_losses[0]

@@ -19,5 +19,5 @@ for v in (0, 3, 5, 7):
         with torch.no_grad():
             out = r.render(cam, model, st)
         torch.cuda.synchronize()
-        print('view', v, 'frame', i, 'window', RZ._DEPTH_WINDOW.get(dev), 'backoff', RZ._MSD_BACKOFF.get(dev, 0), flush=True)
+        print('view', v, 'frame', i, 'window', RZ._window_for(dev), 'backoff', RZ._MSD_BACKOFF.get(dev, 0), flush=True)
     # bucket sizes from the keys of the last frame
