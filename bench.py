@@ -262,9 +262,10 @@ def main():
         t_ms = sum(bwd_live) / len(bwd_live) if dom == "blend_bwd" and bwd_live else stages[dom]
         ach = kern[dom][0] / (t_ms * 1e-3) / 1e9
         copy_gbs = copy_peak_gbs(dev)
-        traffic, tnote = pmc_traffic(dom)
+        traffic, tinfo = pmc_traffic(dom)
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tnote,
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_raw": tinfo.get("traffic_raw"), "traffic_source": tinfo,
                 "avg_launch_ms": round(t_ms, 4), "algorithmic_bytes_per_launch": int(kern[dom][0]),
                 "bytes_model": "44 R + 36 H W + 40 M (SURVEY 8d)" if dom == "blend_bwd"
                 else "44 R + 8 tiles + 28 H W (SURVEY 8d)",
@@ -313,6 +314,11 @@ def main():
             "cpu_baseline": cpu,
             "psnr_vs_ref": psnr,
         }
+        if reducer is not None:
+            nsteps = a.spinup_steps + a.warmup + a.steps + a.diag_steps
+            line["allreduce"] = {"ranges_per_step": reducer.overlap_chunks(), "pipelined_adam": opt is not None,
+                                 "host_us_per_step": {k: round(1e6 * v / nsteps, 1) for k, v in reducer.host_s.items()},
+                                 "avg": reducer._avg}
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
@@ -321,25 +327,43 @@ def main():
 
 def pmc_traffic(stage):
     """HBM bytes per launch of the stage's kernel from the committed PMC
-    summary of this build (tools/pmc.sh -> profiles/pmc_current.txt), as
+    summary (tools/pmc_run.sh -> profiles/pmc_current.txt), as
     MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE doubled (gfx950
-    tallies 128-B read requests at 64 B) + WRITE_SIZE, KiB -> bytes."""
+    tallies 128-B read requests at 64 B) + WRITE_SIZE, KiB -> bytes; the raw
+    sum beside it.  The summary names the library build (source hash) its
+    counters came from: a summary of another build is flagged and its bytes
+    are not reported as this build's traffic."""
     path = os.path.join(ROOT, "profiles", "pmc_current.txt")
     if not os.path.exists(path):
-        return None, None
-    want, cur, vals = "k_" + stage, None, {}
+        return None, {"source": None, "note": "no PMC summary"}
+    sys.path.insert(0, os.path.join(ROOT, "mini-3d-gaussian-splatting_amd"))
+    import build as _build
+    want, cur, vals, pmc_build = "k_" + stage, None, {}, None
     for line in open(path):
-        if line and not line[0].isspace():
+        if line.startswith("#"):
+            parts = line.split()
+            if len(parts) == 3 and parts[1] == "library_source_sha256":
+                pmc_build = parts[2]
+        elif line and not line[0].isspace():
             cur = line.strip()
         elif cur == want:
             parts = line.split()
             if len(parts) == 2:
                 vals[parts[0]] = float(parts[1])
     if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
-        return None, None
-    return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), \
-        (f"profiles/pmc_current.txt: 2 x FETCH_SIZE ({vals['FETCH_SIZE'] * 1024 / 1e6:.1f} MB raw) + WRITE_SIZE "
-         f"({vals['WRITE_SIZE'] * 1024 / 1e6:.1f} MB), rocprofv3 --pmc, one pass each")
+        return None, {"source": "profiles/pmc_current.txt", "note": f"no FETCH/WRITE for {want}"}
+    bench_build = _build.source_hash()
+    fetch, write = vals["FETCH_SIZE"] * 1024, vals["WRITE_SIZE"] * 1024
+    info = {"source": "profiles/pmc_current.txt (rocprofv3 --pmc, one counter group per pass)",
+            "pmc_build": pmc_build, "bench_build": bench_build, "build_match": pmc_build == bench_build,
+            "fetch_raw": int(fetch), "write": int(write), "traffic_raw": int(fetch + write),
+            "correction": "traffic = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: gfx950 counts a 128-B "
+                          "read request as 64 B; stated there for coalesced streaming reads, this kernel's "
+                          "reads are record gathers, so traffic_raw is the lower bound)"}
+    if not info["build_match"]:
+        info["note"] = "stale: the PMC summary is of another library build; traffic not reported"
+        return None, info
+    return int(2 * fetch + write), info
 
 
 def cpu_baseline(scene, W, H, cot, threads):

@@ -29,6 +29,17 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-function"]
 
 
+def source_hash() -> str:
+    """sha256 (16 hex digits) of the library's sources and headers: names the
+    build that measurements (the PMC summary) were taken on."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in SRC + HDR:
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def stale() -> bool:
     if not os.path.exists(OUT):
         return True

@@ -1214,6 +1214,9 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
 #ifndef GS_BWD_CHUNK_STAGE
 #define GS_BWD_CHUNK_STAGE 1
 #endif
+#ifndef GS_BWD_RECENTER  // phase-B row moments about the row nearest each mean (numerics; 0 = about row 0)
+#define GS_BWD_RECENTER 1
+#endif
 constexpr int kBwdGroup = GS_BWD_GROUP;  // live entries per phase-B group: 8 or 4
 static_assert(kBwdGroup == 8 || kBwdGroup == 4, "phase B maps 8 or 16 lanes to an entry");
 constexpr int kBwdLanes = kWave / kBwdGroup;  // lanes per entry in phase B (8 or 16)
@@ -1373,30 +1376,52 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       const float2 ib = s_wrec[6 * e + 2];                                // qo o
       const uint32_t slot = __float_as_uint(s_wrec[6 * e + 5].x);
       const float hop = -0.5f * ib.y;
-      // this lane's pixels (x0 + col, y0 + r), r = 0..7: dx = bx, dy = by + r
-      const float bx = (float)(x0 + col) - ia.x, by = (float)(y0 + row0) - ia.y;
+      // this lane's pixels (x0 + col, y0 + r): dx = bx, dy = by + (r - rc).
+      // The row moments are taken about row rc of the column.  rc = 0 (moments
+      // with constant weights r, r^2) unless the chunk holds a Gaussian with
+      // sigma_y < 2 px: then rc is the column row nearest each mean (clamped),
+      // else such a Gaussian's dy^2 sum cancels -- by^2 S0 + 2 by Soy + Soyy
+      // with |by| up to 7 for a result of ~(0.05)^2 S0: 1e4 x fp32 rounding,
+      // 1.7e-4 of the tensor's scale measured on a sub-pixel Gaussian (2e-6
+      // recentred).  Always recentring cost +28 us per C3 step, this test +7.
+      const float bx = (float)(x0 + col) - ia.x;
+      const float q01h = 0.5f * ib.x;
+      const bool small_y = ia.z < 4.f * (ia.z * ia.w - q01h * q01h);  // Sigma_yy = q00 / det < 4
       float S0 = 0.f, Soy = 0.f, Soyy = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
+      float rc = 0.f;
+      auto moments = [&](auto recenter_tag) {
+        constexpr bool kRec = decltype(recenter_tag)::value;
+        if constexpr (kRec)
+          rc = __builtin_amdgcn_fmed3f(__builtin_rintf((ia.y - (float)(y0 + row0)) * (1.f / kBwdStep)), 0.f,
+                                       (float)(kBwdGroup - 1)) * kBwdStep;
 #pragma unroll
-      for (int r = 0; r < kBwdGroup; ++r) {
-        const int p = col + 8 * (row0 + kBwdStep * r);  // phase A's lane of that pixel
-        const float2 dc = s_dc[j][p];
-        const float dop = dc.x, cs = dc.y;
-        const float4 pg = s_pg[p];
-        // dL/ds: none where the weight clamp bound (sign bit of c) or the pair
-        // was skipped (dop = 0 then); a simple entry's clamps never bind
-        const float ds = kMasked ? (cs > 0.f ? hop * dop : 0.f) : hop * dop;
-        const float cw = fabsf(cs);
-        S0 += ds;
-        if (r) {
-          Soy = __builtin_fmaf(ds, (float)(kBwdStep * r), Soy);
-          Soyy = __builtin_fmaf(ds, (float)(kBwdStep * kBwdStep * r * r), Soyy);
+        for (int r = 0; r < kBwdGroup; ++r) {
+          const int p = col + 8 * (row0 + kBwdStep * r);  // phase A's lane of that pixel
+          const float2 dc = s_dc[j][p];
+          const float dop = dc.x, cs = dc.y;
+          const float4 pg = s_pg[p];
+          // dL/ds: none where the weight clamp bound (sign bit of c) or the pair
+          // was skipped (dop = 0 then); a simple entry's clamps never bind
+          const float ds = kMasked ? (cs > 0.f ? hop * dop : 0.f) : hop * dop;
+          const float cw = fabsf(cs);
+          S0 += ds;
+          if constexpr (kRec) {
+            const float w = (float)(kBwdStep * r) - rc;  // exact: small integers
+            Soy = __builtin_fmaf(ds, w, Soy);
+            Soyy = __builtin_fmaf(ds, w * w, Soyy);
+          } else if (r) {
+            Soy = __builtin_fmaf(ds, (float)(kBwdStep * r), Soy);
+            Soyy = __builtin_fmaf(ds, (float)(kBwdStep * kBwdStep * r * r), Soyy);
+          }
+          g5 += dop;
+          g6 = __builtin_fmaf(pg.x, cw, g6);
+          g7 = __builtin_fmaf(pg.y, cw, g7);
+          g8 = __builtin_fmaf(pg.z, cw, g8);
+          g9 = __builtin_fmaf(pg.w, cw, g9);
         }
-        g5 += dop;
-        g6 = __builtin_fmaf(pg.x, cw, g6);
-        g7 = __builtin_fmaf(pg.y, cw, g7);
-        g8 = __builtin_fmaf(pg.z, cw, g8);
-        g9 = __builtin_fmaf(pg.w, cw, g9);
-      }
+      };
+      if (GS_BWD_RECENTER && wave_any(small_y)) moments(std::true_type{}); else moments(std::false_type{});
+      const float by = (float)(y0 + row0) + rc - ia.y;
       // sums of ds dx, ds dy, ds dx^2, ds dx dy, ds dy^2 over the lane's column
       float Sx = bx * S0, Sy = __builtin_fmaf(by, S0, Soy);
       float g2 = bx * Sx, g3 = bx * Sy;
@@ -1728,7 +1753,12 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd_grp(gs_blend_bwd_args a) {
             const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * j];  // mx my q00 q11
             const float2 ib = s_wrec[6 * j + 2];                                // qo o
             const float hop = -0.5f * ib.y;
-            const float bx = (float)(x0 + col) - ia.x, by = (float)(y0 + row0) - ia.y;
+            const float bx = (float)(x0 + col) - ia.x;  // (row moments about rc: k_blend_bwd)
+            const float rc = GS_BWD_RECENTER ? __builtin_amdgcn_fmed3f(__builtin_rintf((ia.y - (float)(y0 + row0)) *
+                                                                                        (1.f / kBwdStep)),
+                                                                       0.f, (float)(kBwdGroup - 1)) * kBwdStep
+                                             : 0.f;
+            const float by = (float)(y0 + row0) + rc - ia.y;
             float S0 = 0.f, Soy = 0.f, Soyy = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
 #pragma unroll
             for (int r = 0; r < kBwdGroup; ++r) {
@@ -1739,10 +1769,9 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd_grp(gs_blend_bwd_args a) {
               const float ds = kMasked ? (csg > 0.f ? hop * dop : 0.f) : hop * dop;
               const float cw = fabsf(csg);
               S0 += ds;
-              if (r) {
-                Soy = __builtin_fmaf(ds, (float)(kBwdStep * r), Soy);
-                Soyy = __builtin_fmaf(ds, (float)(kBwdStep * kBwdStep * r * r), Soyy);
-              }
+              const float w = (float)(kBwdStep * r) - rc;
+              Soy = __builtin_fmaf(ds, w, Soy);
+              Soyy = __builtin_fmaf(ds, w * w, Soyy);
               g5 += dop;
               g6 = __builtin_fmaf(pg.x, cw, g6);
               g7 = __builtin_fmaf(pg.y, cw, g7);

@@ -27,6 +27,7 @@ at world 8, so one range stays the default (GS_ALLREDUCE_CHUNKS overrides).
 from __future__ import annotations
 
 import os
+import time
 from typing import Iterable, List, Optional
 
 import torch
@@ -63,6 +64,7 @@ class GradAllReduce:
         self._coalesce = (os.environ.get("GS_ALLREDUCE_COALESCE", "1") != "0" and hasattr(dist, "is_initialized")
                           and dist.is_initialized() and dist.get_backend(group) == "nccl")
         self.ranges_reduced = 0  # rows_ready calls so far (diagnostic)
+        self.host_s = {"rows_ready": 0.0, "reduce_and_step": 0.0}  # host seconds spent issuing (diagnostic)
         # RCCL (backend "nccl") forms the mean inside the reduction (ReduceOp.AVG,
         # NCCL >= 2.10); gloo has no AVG: SUM, then one division.  Decided once.
         self._avg: bool = (dist.is_initialized() and dist.get_backend(group) == "nccl"
@@ -93,6 +95,13 @@ class GradAllReduce:
     def rows_ready(self, lo: int, hi: int) -> None:
         """Gradient rows [lo, hi) of every parameter are final in the bucket
         (queued on the current stream): reduce them asynchronously."""
+        t0 = time.perf_counter()
+        try:
+            self._rows_ready(lo, hi)
+        finally:
+            self.host_s["rows_ready"] += time.perf_counter() - t0
+
+    def _rows_ready(self, lo: int, hi: int) -> None:
         flat = self._bucket()
         n = self.params[0].shape[0]
         op = self.dist.ReduceOp.AVG if self._avg else self.dist.ReduceOp.SUM
@@ -180,6 +189,13 @@ class GradAllReduce:
         range k's all-reduce only (FusedAdam.step_ranges), so it overlaps the
         reductions of the later ranges.  Bit-identical to the unpipelined
         sequence (the same reduced values, an elementwise update)."""
+        t0 = time.perf_counter()
+        try:
+            self._reduce_and_step(optimizer)
+        finally:
+            self.host_s["reduce_and_step"] += time.perf_counter() - t0
+
+    def _reduce_and_step(self, optimizer) -> None:
         flat = self._bucket()
         views = torch.split(flat, self._sizes)
         pipelined = (len(self._works) > 1 and hasattr(optimizer, "step_ranges")

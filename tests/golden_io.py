@@ -154,6 +154,14 @@ def grad_rel_err(d, dref, rows=None):
     return max_err(d, dref) / scale
 
 
+def flipped_pixels(out, ref, edge, img_tol=1e-5, alpha_tol=1e-6):
+    """[H,W] bool: knife-edge pixels (`edge`) whose image or alpha differ by
+    more than rounding -- a decision there went the other way."""
+    img = np.abs(np.asarray(out["image"], np.float64) - np.asarray(ref["image"], np.float64)).max(0) > img_tol
+    alp = (np.abs(np.asarray(out["alpha"], np.float64) - np.asarray(ref["alpha"], np.float64)) > alpha_tol)[0]
+    return np.asarray(edge, bool) & (img | alp)
+
+
 def touching_gaussians(means2d, conics, vis, pixels, s_max=23.1 * 1.01):
     """[N] bool: visible Gaussians whose blend footprint (s = d^T Q d <=
     s_max, the :336 skip with a 1 % margin) covers any of `pixels` [(y, x)]."""

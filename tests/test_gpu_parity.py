@@ -293,6 +293,9 @@ def test_depth_sort_msd_overflow_falls_back(pkg, cuda):
     st = pkg.RenderSettings(image_height=H, image_width=W, bg_color=torch.zeros(3))
     r = pkg.GaussianRenderer()
     RZ._MSD_BACKOFF.clear()
+    # (earlier tests' scenes may have switched the depth-key windows off: start clean)
+    RZ._WINDOW_STATE.pop(model._xyz.device, None)
+    RZ._DEPTH_HIST.pop(model._xyz.device, None)
     try:
         with torch.no_grad():
             outs = [r.render(cam, model, st)["image"].clone() for _ in range(3)]  # windowed keys + overflow
@@ -464,14 +467,20 @@ def _scene_vs_oracle(pkg, cuda, sc, W, H, bg, seed=1, renderer_kw=None, knife=Tr
               f"alpha {o['alpha'][0, y, x]:.7f} vs {ref['alpha'][0, y, x]:.7f}; margins w {ref['margin'][0, y, x]:.3g} "
               f"ulps, A {ref['margin'][1, y, x]:.3g} ulps")
     print(f"{label}: {int(bad.sum())} of {H * W} px out of tolerance, {int((bad & edge).sum())} of them knife-edge; "
-          f"knife-edge px overall {int(edge.sum())}; T={ref['T']} E={ref['E']} C={ref['C']}")
+          f"knife-edge px overall {int(edge.sum())}, flipped {int(G.flipped_pixels(o, ref, edge).sum())}; "
+          f"T={ref['T']} E={ref['E']} C={ref['C']}")
     errs = G.check_image(o, ref, exempt=edge if knife else None) + G.check_projection(o, ref)
     ds, dr = G.oracle().covariance_backward(sc.scaling.numpy(), sc.rotation.numpy(), ref["grads"]["cov3d"])
     op = torch.sigmoid(sc.opacity[:, 0]).numpy()
-    # Gradients: a flipped knife-edge pixel changes the gradient of every
-    # Gaussian in its chain; those Gaussians (footprint covering the pixel)
-    # are exempt from the 1e-4 check and reported beside the others
-    flipped = list(zip(*np.nonzero(bad & edge))) if knife else []
+    # Gradients: a knife-edge pixel whose decision flipped changes the
+    # gradient of every Gaussian in its chain; those Gaussians (footprint
+    # covering the pixel) are exempt from the 1e-4 check and reported beside
+    # the others.  Flipped = knife-edge and visibly different: image > 1e-5 or
+    # alpha > 1e-6 (rounding differences are ~1e-7; a flip past the last
+    # contributor moves A by that contributor's c, which may stay under the
+    # 1e-4 image tolerance)
+    flipped = G.flipped_pixels(o, ref, edge) if knife else np.zeros_like(edge)
+    flipped = list(zip(*np.nonzero(flipped)))
     touch = G.touching_gaussians(o["means2d"], o["conics"], o["vis"], flipped)
     rows = ~touch
     pairs = (("xyz", _np(m._xyz.grad), ref["grads"]["xyz"]), ("scaling", _np(m._scaling.grad), ds),
@@ -720,14 +729,16 @@ def test_depth_window_miss_rerenders(pkg, cuda):
             assert torch.equal(a, b)
         for a, b in zip(fresh_narrow, held_narrow):
             assert torch.equal(a, b)
-        # once the wide frame has left the history, it misses again; a second
-        # miss within _MISS_SPAN frames switches the windows off
+        # the wide frame misses a narrow-only history; once it has left the
+        # history again it misses again, and a second miss within _MISS_SPAN
+        # frames switches the windows off
+        again = frame(wide)                  # miss 1 after the reset
         for _ in range(RZ._WINDOW_FRAMES):
             frame(narrow)
-        again = frame(wide)
+        again2 = frame(wide)                 # miss 2, RZ._WINDOW_FRAMES + 1 frames later
         assert misses() == 2 and RZ._window_for(cuda) is None
-        for a, b in zip(fresh_wide, again):
-            assert torch.equal(a, b)
+        for a, b, c in zip(fresh_wide, again, again2):
+            assert torch.equal(a, b) and torch.equal(a, c)
     finally:
         reset()
 

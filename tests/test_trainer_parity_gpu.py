@@ -167,6 +167,12 @@ def test_trainer_steps_match_composed_step(pkg, cuda, tmp_path, reset_adam):
                              position_lr_init=1.6e-3, position_lr_final=1.6e-5, reset_adam_on_densify=reset_adam)
     tr = pkg.GaussianTrainer(cfg, ds)
     tr.setup()
+    # create_from_random makes every Gaussian isotropic (gaussian_model.py:78-98),
+    # where dL/drotation is zero up to rounding: make them anisotropic, so that
+    # the rotation gradients compared are well conditioned
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(5)
+        tr.gaussians._scaling.add_(torch.empty(tr.gaussians._scaling.shape).uniform_(-0.7, 0.7, generator=g).to(cuda))
     init = [q.detach().cpu().clone() for q in tr.gaussians.parameter_list()]
     cams, perm, extent = ds.get_train_cameras(), tr._perm, tr.scene_extent
 
