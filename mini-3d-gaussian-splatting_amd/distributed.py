@@ -1,28 +1,31 @@
-"""Data-parallel training over views: one view per GPU, one all-reduce.
+"""Data-parallel training over views: one view per GPU, one gradient mean.
 
 SURVEY.md 8(e): each rank renders its own camera with a full replica of the
 GaussianModel; the only exchange per step is the mean of the Gaussian
-parameter gradients, done as ONE flat all_reduce(SUM) / world over
-torch.distributed (backend "nccl" = RCCL over xGMI on MI355X, "gloo" on CPU
-for tests), before optimizer.step().  Payload: xyz 3 + features_dc 3 +
-scaling 3 + rotation 4 + opacity 1 = 14 fp32 (56 B) per Gaussian;
-features_rest has an identically zero render gradient and is not sent unless
-SH colour is on (GaussianModel.grad_parameters: +45 fp32 per Gaussian then).
+parameter gradients before the optimizer step.  Payload: xyz 3 + features_dc
+3 + scaling 3 + rotation 4 + opacity 1 = 14 fp32 (56 B) per Gaussian, one
+flat bucket; features_rest has an identically zero render gradient and is not
+sent unless SH colour is on (GaussianModel.grad_parameters: +45 fp32 then).
 
-Overlap: with the bucket attached (zero copy), the render backward runs its
-last stage (gradient gather + projection backward) in `chunks` ranges of
+Transport: backend "nccl" (= RCCL over xGMI on MI355X) goes to RCCL directly
+(rccl.RcclComm: a communicator of its own, its own HIP stream, ncclAvg, per
+range an event pair), because torch.distributed's per-call host time (22 us
+an all-reduce, 59 us a coalesced group, 9 us an event) set the pace of the
+step's tail; GS_DP_NATIVE=0 keeps torch.distributed.  gloo (CPU tests) sums,
+then divides by the world size.
+
+Pipelining: with the bucket attached (zero copy), the render backward runs
+its last stage (gradient gather + projection backward) in `chunks` ranges of
 Gaussians and hands each finished range to rows_ready(), which issues its
-all-reduces asynchronously (RCCL's own stream waits for the range's kernels
-only): range k's reduction runs while range k+1 is computed.
-all_reduce_mean() then waits for them.  Every rank issues the same ranges in
-the same order (same N, same chunk rule), as collectives must match.  The
-default is one range (one all_reduce call over the whole bucket, issued the
-moment the backward's last kernel is queued).  A range below the whole is
-one coalesced collective over its five parameter slices (RCCL group launch;
-five separate calls cost ~25-30 us of host time each): measured at world
-size 1, two ranges cost ~70 us more per step than one (four: ~160 us),
-about what a second range could hide behind the gather + projection backward
-at world 8, so one range stays the default (GS_ALLREDUCE_CHUNKS overrides).
+reduction asynchronously (the collective stream waits for that range's
+kernels only); reduce_and_step() then queues the Adam update of range k
+behind range k's reduction only (FusedAdam.step_ranges), so range k's
+reduction overlaps the gather / projection backward of the ranges after it
+and the Adam updates of the ranges before it.  Every rank issues the same
+ranges in the same order (same N, same chunk rule), as collectives must
+match.  Default: 4 ranges above one rank, 1 at world size 1
+(GS_ALLREDUCE_CHUNKS overrides); the result is bit-identical for every range
+count (an elementwise update of the same reduced values).
 """
 from __future__ import annotations
 
@@ -31,6 +34,25 @@ import time
 from typing import Iterable, List, Optional
 
 import torch
+
+
+_NATIVE_COMMS: dict = {}
+
+
+def _native_comm(dist, group):
+    """The process group's RcclComm on the current device (created once, on
+    every rank together: the first GradAllReduce is built at the same
+    iteration everywhere), or None if RCCL cannot be driven directly."""
+    key = (id(group if group is not None else dist.group.WORLD), torch.cuda.current_device())
+    if key not in _NATIVE_COMMS:
+        try:
+            from .rccl import RcclComm
+            _NATIVE_COMMS[key] = RcclComm(dist, group)
+        except Exception as e:  # e.g. no librccl beside torch: the torch.distributed path
+            import warnings
+            warnings.warn(f"native RCCL unavailable ({e}); gradient all-reduce through torch.distributed")
+            _NATIVE_COMMS[key] = None
+    return _NATIVE_COMMS[key]
 
 
 class GradAllReduce:
@@ -53,10 +75,18 @@ class GradAllReduce:
         self._sizes: List[int] = []
         # overlap ranges: `chunks` when every range keeps >= min_chunk_rows
         # Gaussians (smaller launches would not fill the GPU)
-        # default 1: measured on the box (RCCL, world size 1), every all_reduce call
-        # costs ~25-30 us of host time the GPU then waits for; with one range the
-        # whole bucket goes in one call, issued as soon as the backward is queued
-        self.chunks = int(chunks if chunks is not None else os.environ.get("GS_ALLREDUCE_CHUNKS", 1))
+        # default: 4 ranges above one rank (each range's reduction overlaps the
+        # gather / projection backward of the ranges after it, and its Adam
+        # update the reductions after it: GradAllReduce.reduce_and_step), 1 at
+        # world size 1.  Through native RCCL a range costs ~32 us of host time
+        # and ~10 us of GPU time more than one whole-bucket call (world-size-1
+        # rehearsal, profiles/r03/dist/); through torch.distributed's coalescing
+        # manager it was ~70 us.
+        if chunks is None:
+            env = os.environ.get("GS_ALLREDUCE_CHUNKS")
+            world = dist.get_world_size(group) if (hasattr(dist, "is_initialized") and dist.is_initialized()) else 1
+            chunks = int(env) if env else (4 if world > 1 else 1)
+        self.chunks = int(chunks)
         self.min_chunk_rows = int(min_chunk_rows if min_chunk_rows is not None
                                   else os.environ.get("GS_ALLREDUCE_MIN_ROWS", 1 << 16))
         self._works: list = []
@@ -69,6 +99,11 @@ class GradAllReduce:
         # NCCL >= 2.10); gloo has no AVG: SUM, then one division.  Decided once.
         self._avg: bool = (dist.is_initialized() and dist.get_backend(group) == "nccl"
                            and hasattr(dist.ReduceOp, "AVG")) if hasattr(dist, "is_initialized") else False
+        # backend "nccl": the collectives go to RCCL directly (rccl.RcclComm, one
+        # communicator per process group and device, ncclAvg), unless GS_DP_NATIVE=0
+        self._native = None
+        if self._avg and os.environ.get("GS_DP_NATIVE", "1") != "0":
+            self._native = _native_comm(dist, group)
 
     def _bucket(self) -> torch.Tensor:
         sizes = [p.numel() for p in self.params]
@@ -106,6 +141,20 @@ class GradAllReduce:
         n = self.params[0].shape[0]
         op = self.dist.ReduceOp.AVG if self._avg else self.dist.ReduceOp.SUM
         self.ranges_reduced += 1
+        if self._native is not None:
+            # the range's slice of every parameter (the whole bucket: one piece)
+            if lo == 0 and hi == n:
+                pieces = [(flat.data_ptr(), flat.numel())]
+            else:
+                pieces, off = [], 0
+                for size in self._sizes:
+                    cols = size // n
+                    pieces.append((flat.data_ptr() + 4 * (off + lo * cols), (hi - lo) * cols))
+                    off += size
+            k = len(self._works)
+            self._native.all_reduce(k, pieces, avg=True)
+            self._works.append((lo, hi, k))
+            return
         if lo == 0 and hi == n:  # every row: the whole bucket in one call
             self._works.append((lo, hi, [self.dist.all_reduce(flat, op=op, group=self.group, async_op=True)]))
             return
@@ -155,8 +204,7 @@ class GradAllReduce:
         if self._works:
             # the backward reduced the bucket range by range (rows_ready)
             for _, _, ws in self._works:
-                for w in ws:
-                    w.wait()
+                self._wait(ws)
             self._works = []
             if not self._avg:
                 flat.div_(self.dist.get_world_size(self.group))
@@ -169,6 +217,10 @@ class GradAllReduce:
             else:
                 v.copy_(p.grad.reshape(-1))
         world = self.dist.get_world_size(self.group)
+        if self._native is not None:
+            self._native.all_reduce(0, [(flat.data_ptr(), flat.numel())], avg=True)
+            self._native.wait(0)
+            return self._copy_out(views, in_place)
         if self._avg:
             # RCCL divides inside the reduction: no extra pass over the bucket
             try:
@@ -210,12 +262,20 @@ class GradAllReduce:
 
         def before(k):
             lo, hi, ws = works[k]
-            for w in ws:
-                w.wait()  # (RCCL: the current stream waits for this range's collective)
+            self._wait(ws)  # (RCCL: the current stream waits for this range's collective)
             if not self._avg:
                 for v in views:
                     v.view(n, -1)[lo:hi].div_(world)
         optimizer.step_ranges([(lo, hi) for lo, hi, _ in works], before)
+
+    def _wait(self, ws) -> None:
+        """Make the current stream wait for one range's collective(s): torch
+        Work objects, or the native communicator's range index."""
+        if isinstance(ws, int):
+            self._native.wait(ws)
+            return
+        for w in ws:
+            w.wait()
 
     def _copy_out(self, views, in_place) -> None:
         for p, v, ok in zip(self.params, views, in_place):

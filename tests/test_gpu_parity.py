@@ -640,11 +640,16 @@ def test_grad_bucket_adoption(pkg, cuda):
         assert torch.equal(a, b)
 
 
-def test_rccl_range_reduction_world1(pkg, cuda):
+@pytest.mark.parametrize("native", [True, False])
+def test_rccl_range_reduction_world1(pkg, cuda, native, monkeypatch):
     """The RCCL path itself (backend nccl, world size 1, in this process): the
     backward hands its rows over in ranges, each range's five parameter
-    slices reduced as one coalesced collective; the gradients equal a plain
-    backward's bit for bit (a mean over one rank)."""
+    slices reduced as one collective group -- through the native RCCL
+    communicator (rccl.RcclComm) or torch.distributed's coalescing manager --;
+    the gradients equal a plain backward's bit for bit (a mean over one rank),
+    and a pipelined Adam (GradAllReduce.reduce_and_step -> FusedAdam.step_ranges)
+    equals one FusedAdam step on them."""
+    monkeypatch.setenv("GS_DP_NATIVE", "1" if native else "0")
     import os
     import socket
     import torch.distributed as dist
@@ -659,24 +664,34 @@ def test_rccl_range_reduction_world1(pkg, cuda):
     try:
         syn = pkg.synthetic
         sc = syn.make_scene(20000, 320, 240, seed=5)
-        res = []
-        for ranges in (0, 1, 3):
+        res, stepped = [], []
+        for ranges in (0, 1, 3, 3):
             m = syn.to_model(sc, pkg.GaussianModel, cuda)
             params = m.grad_parameters()
+            opt = pkg.optim.FusedAdam([{"params": [p], "lr": 1e-3} for p in params])
             red = None
             if ranges:
                 red = pkg.distributed.GradAllReduce(params, chunks=ranges, min_chunk_rows=4096).attach(m)
-                assert red._coalesce
+                assert red._coalesce and (red._native is not None) == native
             out = pkg.GaussianRenderer().render(Cam(320, 240, sc.fovx, sc.fovy), m,
                                                 pkg.RenderSettings(240, 320, torch.zeros(3)))
             (out["image"].sum() + out["alpha"].sum() + out["depth"].sum()).backward()
             if red is not None:
                 assert red.ranges_reduced == ranges
-                red.all_reduce_mean()
+            if red is not None and len(res) == 3:
+                red.reduce_and_step(opt)  # pipelined: each range's Adam behind its collective
+            else:
+                if red is not None:
+                    red.all_reduce_mean()
+                opt.step()
             torch.cuda.synchronize()
             res.append([p.grad.clone() for p in params])
+            stepped.append([p.detach().clone() for p in params])
         for other in res[1:]:
             for a, b in zip(res[0], other):
+                assert torch.equal(a, b)
+        for other in stepped[1:]:
+            for a, b in zip(stepped[0], other):
                 assert torch.equal(a, b)
     finally:
         dist.destroy_process_group()
