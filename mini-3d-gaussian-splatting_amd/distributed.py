@@ -55,6 +55,15 @@ def _native_comm(dist, group):
     return _NATIVE_COMMS[key]
 
 
+def close_native_comms() -> None:
+    """Destroy the native RCCL communicators (before the process group goes:
+    every rank calls it at the same point, after its last collective)."""
+    for key, comm in list(_NATIVE_COMMS.items()):
+        if comm is not None:
+            comm.close()
+        del _NATIVE_COMMS[key]
+
+
 class GradAllReduce:
     """Mean-all-reduce of `params`' .grad through one flat bucket.
 

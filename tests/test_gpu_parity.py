@@ -694,6 +694,7 @@ def test_rccl_range_reduction_world1(pkg, cuda, native, monkeypatch):
             for a, b in zip(stepped[0], other):
                 assert torch.equal(a, b)
     finally:
+        pkg.distributed.close_native_comms()
         dist.destroy_process_group()
 
 
