@@ -1930,10 +1930,12 @@ __device__ __forceinline__ float lanes_sum(float v) {
 #ifndef GS_GATHER_HL1
 #define GS_GATHER_HL1 4
 #endif
+
 constexpr int kGatherHL1 = GS_GATHER_HL1;  // slot lanes per Gaussian with one partial group per slot
 
-template <int QL, int HL>
-__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng) {
+template <int QL, int HL, int kNG = 0>  // kNG > 0: the partial groups per slot at compile time (else ng)
+__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng_rt) {
+  const uint32_t ng = kNG > 0 ? (uint32_t)kNG : ng_rt;
   constexpr int LPG = QL * HL;
   static_assert(LPG == 2 || LPG == 4 || LPG == 8, "lanes per Gaussian");
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
@@ -1982,6 +1984,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float *src = reinterpret_cast<const float *>(part + (size_t)(e0 + HL * i) * ng * kF2);
+        // (non-temporal loads, for data read once, measured +10 us: profiles/r03/experiments.md)
         va[i] = f[i] ? *reinterpret_cast<const f4_u8 *>(src) : f4_u8{0.f, 0.f, 0.f, 0.f};
         vb[i] = f[i] ? *reinterpret_cast<const f4_u8 *>(src + 4) : f4_u8{0.f, 0.f, 0.f, 0.f};
         vc[i] = f[i] ? *reinterpret_cast<const f2_u8 *>(src + 8) : f2_u8{0.f, 0.f};
@@ -2583,6 +2586,8 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
       k_gather_slots<1, kGatherHL1><<<div_up((long long)kGatherHL1 * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
     else if (ng == 2)
       k_gather_slots<2, 2><<<div_up(4LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
+    else if (ng == 4)  // the default tile's four cells
+      k_gather_slots<4, 2, 4><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
     else
       k_gather_slots<4, 2><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
   }
