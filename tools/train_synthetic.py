@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--views", type=int, default=100)
     ap.add_argument("--size", type=int, default=800)
     ap.add_argument("--gt-gaussians", type=int, default=200_000)
+    ap.add_argument("--profile-iters", type=int, default=0,
+                    help="host profile (cProfile) of this many iterations after 100 warm ones, then exit")
     a = ap.parse_args()
     import __graft_entry__ as ge
     pkg = ge.load_package()
@@ -63,6 +65,21 @@ def main():
                              densify_until_iter=min(15000, a.iters // 2), output_path=os.path.join(tmp, "out"))
     tr = pkg.GaussianTrainer(cfg, ds)
     tr.setup()
+    if a.profile_iters:
+        import cProfile
+        import pstats
+        tr.train(100)
+        torch.cuda.synchronize()
+        pr = cProfile.Profile()
+        t0 = time.perf_counter()
+        pr.enable()
+        tr.train(a.profile_iters)
+        torch.cuda.synchronize()
+        pr.disable()
+        dt = time.perf_counter() - t0
+        print(f"{a.profile_iters} iterations: {1e3 * dt / a.profile_iters:.3f} ms each (with the profiler)")
+        pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+        return
     p0 = tr.validate()["psnr"]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
