@@ -1,17 +1,22 @@
 // gs_loss.hip -- fused L1 + D-SSIM photometric loss, forward and backward
 // (include/gsplat_mi355x.h, "Photometric loss").
 //
-// Forward, one 256-thread workgroup per 16x16 output tile of one channel:
-// the (16+2R)^2 patch of pred and target goes to LDS (zero outside the
-// image = the reference's conv2d zero padding), a horizontal pass forms the
-// five windowed sums (x, y, x^2, y^2, xy) per patch row, a vertical pass the
-// per-pixel statistics.  Each pixel then has its SSIM, |x - y| and the three
-// partial derivatives of its clamped SSIM with respect to (mu_x, E[x^2],
-// E[xy]); the workgroup writes its two partial sums (fixed-order tree), and
-// a one-workgroup kernel reduces them in fixed order, in double.
+// Forward, one 256-thread workgroup per 32x32 output tile of one channel:
+// the (32+2R)^2 patch of pred and target goes to LDS (zero outside the
+// image = the reference's conv2d zero padding).  A horizontal pass forms the
+// five windowed sums (x, y, x^2, y^2, xy) per patch row, each thread item
+// sliding over 4 adjacent outputs from registers; a vertical pass gives every
+// thread one column of 4 output rows, again from registers.  The taps of
+// every sum are accumulated in window order (fma), as a single-output loop
+// would.  Each pixel then has its SSIM, |x - y| and the three partial
+// derivatives of its clamped SSIM with respect to (mu_x, E[x^2], E[xy]); the
+// workgroup writes its two partial sums (fixed-order tree), and a
+// one-workgroup kernel reduces them in fixed order, in double.
 // Backward: dL/dx_p = blur(m1)(p) + 2 x_p blur(m2)(p) + y_p blur(m3)(p)
 // (the window is symmetric, so the adjoint of the zero-padded blur is the
 // same blur), scaled by -lambda / (CHW), plus (1 - lambda) sign(x - y) / (CHW).
+// Kernels are instantiated per window radius (taps unrolled, weights in
+// registers).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -21,10 +26,16 @@
 
 namespace {
 
-constexpr int kT = 16;                       // output tile edge
-constexpr int kThreads = kT * kT;            // 256
+constexpr int kTW = 32;                      // output tile width
+constexpr int kTH = 32;                      // output tile height
+constexpr int kThreads = 256;
+constexpr int kRows = kTW * kTH / kThreads;  // vertical pass: output rows per thread
+constexpr int kSeg = 4;                      // horizontal pass: outputs per thread item
+constexpr int kSegs = kTW / kSeg;
 constexpr int kMaxR = GS_LOSS_MAX_WINDOW / 2;
-constexpr int kP = kT + 2 * kMaxR;           // patch edge at the largest window
+static_assert(kThreads % kTW == 0 && kRows * kThreads == kTW * kTH, "tile / block shape");
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 struct Window {
   float w[GS_LOSS_MAX_WINDOW];
@@ -42,70 +53,144 @@ __device__ __forceinline__ float block_sum(float v, float *s_red) {
   return (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
 }
 
+template <int R>
 __global__ __launch_bounds__(kThreads) void k_loss_fwd(gs_loss_args a, Window win, float2 *partials) {
-  __shared__ float sx[kP][kP + 1], sy[kP][kP + 1];
-  __shared__ float sh[5][kP][kT + 1];
+  constexpr int K = 2 * R + 1, PH = kTH + 2 * R, PW = kTW + 2 * R;
+  // The patch is held as (x, y) pairs and the row sums as (x, y), (x^2, y^2)
+  // pairs plus xy, so two of every three sums advance by one packed fp32 FMA
+  // (each half an ordinary fp32 fma: the same values as scalar code).  The
+  // patch and the row sums share one LDS buffer: the row sums wait in
+  // registers until every thread has read its patch rows.
+  constexpr int kPatch = 2 * PH * (PW + 1), kSums = 5 * PH * (kTW + 1);
+  __shared__ __attribute__((aligned(16))) float smem[kPatch > kSums ? kPatch : kSums];
   __shared__ float s_red[4];
-  const int H = a.height, W = a.width, c = blockIdx.z, R = win.r, P = kT + 2 * R;
-  const int x0 = blockIdx.x * kT, y0 = blockIdx.y * kT;
+  auto sxy = reinterpret_cast<f2(*)[PW + 1]>(smem);
+  auto s01 = reinterpret_cast<f2(*)[kTW + 1]>(smem);
+  auto s23 = reinterpret_cast<f2(*)[kTW + 1]>(smem + 2 * PH * (kTW + 1));
+  auto s4 = reinterpret_cast<float(*)[kTW + 1]>(smem + 4 * PH * (kTW + 1));
+  float w[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) w[k] = win.w[k];
+  const int H = a.height, W = a.width, c = blockIdx.z;
+  const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
   const size_t plane = (size_t)H * W;
   const float *px = a.pred + c * plane, *py = a.target + c * plane;
-  for (int i = threadIdx.x; i < P * P; i += kThreads) {
-    const int r = i / P, q = i % P, gy = y0 - R + r, gx = x0 - R + q;
-    const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-    sx[r][q] = in ? px[(size_t)gy * W + gx] : 0.f;
-    sy[r][q] = in ? py[(size_t)gy * W + gx] : 0.f;
+  // patch load: every load of the thread in flight before the first LDS store
+  constexpr int kLoads = (PH * PW + kThreads - 1) / kThreads;
+  f2 lxy[kLoads];
+#pragma unroll
+  for (int it = 0; it < kLoads; ++it) {
+    const int i = threadIdx.x + it * kThreads, r = i / PW, q = i - r * PW, gy = y0 - R + r, gx = x0 - R + q;
+    const bool in = i < PH * PW && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    lxy[it].x = in ? px[(size_t)gy * W + gx] : 0.f;
+    lxy[it].y = in ? py[(size_t)gy * W + gx] : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < kLoads; ++it) {
+    const int i = threadIdx.x + it * kThreads, r = i / PW, q = i - r * PW;
+    if (i < PH * PW) sxy[r][q] = lxy[it];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < P * kT; i += kThreads) {  // horizontal pass
-    const int r = i / kT, q = i % kT;
-    float h0 = 0.f, h1 = 0.f, h2 = 0.f, h3 = 0.f, h4 = 0.f;
-    for (int k = 0; k <= 2 * R; ++k) {
-      const float w = win.w[k], u = sx[r][q + k], v = sy[r][q + k];
-      h0 = __builtin_fmaf(w, u, h0);
-      h1 = __builtin_fmaf(w, v, h1);
-      h2 = __builtin_fmaf(w, u * u, h2);
-      h3 = __builtin_fmaf(w, v * v, h3);
-      h4 = __builtin_fmaf(w, u * v, h4);
+  constexpr int kItems = (PH * kSegs + kThreads - 1) / kThreads;
+  f2 hm[kItems][kSeg], hq[kItems][kSeg];  // (sum x, sum y), (sum x^2, sum y^2)
+  float hp[kItems][kSeg];                  // sum xy
+#pragma unroll
+  for (int it = 0; it < kItems; ++it) {  // horizontal pass
+    const int i = threadIdx.x + it * kThreads, r = i / kSegs, q0 = (i % kSegs) * kSeg;
+    if (i >= PH * kSegs) break;
+    f2 v[kSeg + 2 * R], sq[kSeg + 2 * R];
+    float pr[kSeg + 2 * R];
+#pragma unroll
+    for (int j = 0; j < kSeg + 2 * R; ++j) {
+      v[j] = sxy[r][q0 + j];
+      sq[j] = v[j] * v[j];
+      pr[j] = v[j].x * v[j].y;
     }
-    sh[0][r][q] = h0; sh[1][r][q] = h1; sh[2][r][q] = h2; sh[3][r][q] = h3; sh[4][r][q] = h4;
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) {
+      f2 m = {0.f, 0.f}, q2 = {0.f, 0.f};
+      float pp = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const f2 wk = {w[k], w[k]};
+        m = __builtin_elementwise_fma(wk, v[o + k], m);
+        q2 = __builtin_elementwise_fma(wk, sq[o + k], q2);
+        pp = __builtin_fmaf(w[k], pr[o + k], pp);
+      }
+      hm[it][o] = m; hq[it][o] = q2; hp[it][o] = pp;
+    }
+  }
+  const int col = threadIdx.x % kTW, r0 = (threadIdx.x / kTW) * kRows, gx = x0 + col;
+  float xc[kRows], yc[kRows];  // this thread's output pixels, fetched while the row sums settle
+#pragma unroll
+  for (int o = 0; o < kRows; ++o) {
+    const int gy = y0 + r0 + o;
+    const bool in = gy < H && gx < W;
+    xc[o] = in ? px[(size_t)gy * W + gx] : 0.f;
+    yc[o] = in ? py[(size_t)gy * W + gx] : 0.f;
   }
   __syncthreads();
-  const int oy = threadIdx.x / kT, ox = threadIdx.x % kT, gy = y0 + oy, gx = x0 + ox;
-  float mx = 0.f, my = 0.f, exx = 0.f, eyy = 0.f, exy = 0.f;
-  for (int k = 0; k <= 2 * R; ++k) {  // vertical pass
-    const float w = win.w[k];
-    mx = __builtin_fmaf(w, sh[0][oy + k][ox], mx);
-    my = __builtin_fmaf(w, sh[1][oy + k][ox], my);
-    exx = __builtin_fmaf(w, sh[2][oy + k][ox], exx);
-    eyy = __builtin_fmaf(w, sh[3][oy + k][ox], eyy);
-    exy = __builtin_fmaf(w, sh[4][oy + k][ox], exy);
+#pragma unroll
+  for (int it = 0; it < kItems; ++it) {
+    const int i = threadIdx.x + it * kThreads, r = i / kSegs, q0 = (i % kSegs) * kSeg;
+    if (i >= PH * kSegs) break;
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) {
+      s01[r][q0 + o] = hm[it][o];
+      s23[r][q0 + o] = hq[it][o];
+      s4[r][q0 + o] = hp[it][o];
+    }
   }
-  float ssim_c = 0.f, l1 = 0.f;
-  if (gy < H && gx < W) {
-    const float x = sx[oy + R][ox + R], y = sy[oy + R][ox + R];
-    l1 = fabsf(x - y);
+  __syncthreads();
+  f2 am[kRows], aq[kRows];
+  float ap[kRows];
+#pragma unroll
+  for (int o = 0; o < kRows; ++o) {
+    am[o] = aq[o] = (f2){0.f, 0.f};
+    ap[o] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < kRows + 2 * R; ++j) {  // vertical pass: row j feeds output o at tap j - o
+    const f2 m = s01[r0 + j][col], q2 = s23[r0 + j][col];
+    const float pp = s4[r0 + j][col];
+#pragma unroll
+    for (int o = 0; o < kRows; ++o) {
+      const int k = j - o;
+      if (k >= 0 && k < K) {
+        const f2 wk = {w[k], w[k]};
+        am[o] = __builtin_elementwise_fma(wk, m, am[o]);
+        aq[o] = __builtin_elementwise_fma(wk, q2, aq[o]);
+        ap[o] = __builtin_fmaf(w[k], pp, ap[o]);
+      }
+    }
+  }
+  const size_t n = (size_t)a.channels * plane;
+  float ss = 0.f, sl = 0.f;
+#pragma unroll
+  for (int o = 0; o < kRows; ++o) {
+    const int gy = y0 + r0 + o;
+    if (gy >= H || gx >= W) continue;
+    const float mx = am[o].x, my = am[o].y, exx = aq[o].x, eyy = aq[o].y, exy = ap[o];
+    const float x = xc[o], y = yc[o];
+    sl += fabsf(x - y);
     // loss.py:33-38
     const float sxx = exx - mx * mx, syy = eyy - my * my, sxy = exy - mx * my;
     const float A1 = 2.f * mx * my + a.c1, A2 = 2.f * sxy + a.c2;
     const float B1 = mx * mx + my * my + a.c1, B2 = sxx + syy + a.c2;
     const float D = B1 * B2, S = (A1 * A2) / D;
-    ssim_c = fminf(fmaxf(S, 0.f), 1.f);  // loss.py:39 (NaN -> 0 here; torch would keep NaN)
+    ss += fminf(fmaxf(S, 0.f), 1.f);  // loss.py:39 (NaN -> 0 here; torch would keep NaN)
     if (a.maps) {
       // d clamp(S)/dS: 1 on [0,1] (torch clamp_backward, boundary-inclusive), else 0
       const float g = (S >= 0.f && S <= 1.f) ? 1.f : 0.f;
       const float iD = 1.f / D;
-      const float d_mu = g * 2.f * iD * (my * (A2 - A1) - S * mx * (B2 - B1));
-      const float d_exx = g * (-S / B2);
-      const float d_exy = g * 2.f * A1 * iD;
-      const size_t o = c * plane + (size_t)gy * W + gx, n = (size_t)a.channels * plane;
-      a.maps[o] = d_mu;
-      a.maps[n + o] = d_exx;
-      a.maps[2 * n + o] = d_exy;
+      const size_t p = c * plane + (size_t)gy * W + gx;
+      a.maps[p] = g * 2.f * iD * (my * (A2 - A1) - S * mx * (B2 - B1));  // d/d mu_x
+      a.maps[n + p] = g * (-S / B2);                                     // d/d E[x^2]
+      a.maps[2 * n + p] = g * 2.f * A1 * iD;                             // d/d E[xy]
     }
   }
-  const float ss = block_sum(ssim_c, s_red);
-  const float sl = block_sum(l1, s_red);
+  ss = block_sum(ss, s_red);
+  sl = block_sum(sl, s_red);
   if (threadIdx.x == 0)
     partials[((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = make_float2(ss, sl);
 }
@@ -136,50 +221,126 @@ __global__ __launch_bounds__(1024) void k_loss_final(gs_loss_args a, const float
   }
 }
 
+template <int R>
 __global__ __launch_bounds__(kThreads) void k_loss_bwd(gs_loss_args a, Window win) {
-  __shared__ float sm[3][kP][kP + 1];
-  __shared__ float sh[3][kP][kT + 1];
-  const int H = a.height, W = a.width, c = blockIdx.z, R = win.r, P = kT + 2 * R;
-  const int x0 = blockIdx.x * kT, y0 = blockIdx.y * kT;
+  constexpr int K = 2 * R + 1, PH = kTH + 2 * R, PW = kTW + 2 * R;
+  // maps 1 and 2 travel as a pair (packed fp32 FMA), map 3 alone; patch and
+  // row sums share LDS, as in the forward
+  constexpr int kPatch = 3 * PH * (PW + 1), kSums = 3 * PH * (kTW + 1);
+  __shared__ __attribute__((aligned(16))) float smem[kPatch > kSums ? kPatch : kSums];
+  auto sp = reinterpret_cast<f2(*)[PW + 1]>(smem);
+  auto s2 = reinterpret_cast<float(*)[PW + 1]>(smem + 2 * PH * (PW + 1));
+  auto hp = reinterpret_cast<f2(*)[kTW + 1]>(smem);
+  auto h2 = reinterpret_cast<float(*)[kTW + 1]>(smem + 2 * PH * (kTW + 1));
+  float w[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) w[k] = win.w[k];
+  const int H = a.height, W = a.width, c = blockIdx.z;
+  const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
   const size_t plane = (size_t)H * W, n = (size_t)a.channels * plane;
   const float *m = a.maps + c * plane;
-  for (int i = threadIdx.x; i < P * P; i += kThreads) {
-    const int r = i / P, q = i % P, gy = y0 - R + r, gx = x0 - R + q;
-    const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+  constexpr int kLoads = (PH * PW + kThreads - 1) / kThreads;  // all in flight, as in the forward
+  f2 l01[kLoads];
+  float l2[kLoads];
+#pragma unroll
+  for (int it = 0; it < kLoads; ++it) {
+    const int i = threadIdx.x + it * kThreads, r = i / PW, q = i - r * PW, gy = y0 - R + r, gx = x0 - R + q;
+    const bool in = i < PH * PW && gy >= 0 && gy < H && gx >= 0 && gx < W;
     const size_t o = (size_t)gy * W + gx;
-    sm[0][r][q] = in ? m[o] : 0.f;
-    sm[1][r][q] = in ? m[n + o] : 0.f;
-    sm[2][r][q] = in ? m[2 * n + o] : 0.f;
+    l01[it].x = in ? m[o] : 0.f;
+    l01[it].y = in ? m[n + o] : 0.f;
+    l2[it] = in ? m[2 * n + o] : 0.f;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < P * kT; i += kThreads) {
-    const int r = i / kT, q = i % kT;
-    float h0 = 0.f, h1 = 0.f, h2 = 0.f;
-    for (int k = 0; k <= 2 * R; ++k) {
-      const float w = win.w[k];
-      h0 = __builtin_fmaf(w, sm[0][r][q + k], h0);
-      h1 = __builtin_fmaf(w, sm[1][r][q + k], h1);
-      h2 = __builtin_fmaf(w, sm[2][r][q + k], h2);
+#pragma unroll
+  for (int it = 0; it < kLoads; ++it) {
+    const int i = threadIdx.x + it * kThreads, r = i / PW, q = i - r * PW;
+    if (i < PH * PW) {
+      sp[r][q] = l01[it];
+      s2[r][q] = l2[it];
     }
-    sh[0][r][q] = h0; sh[1][r][q] = h1; sh[2][r][q] = h2;
   }
   __syncthreads();
-  const int oy = threadIdx.x / kT, ox = threadIdx.x % kT, gy = y0 + oy, gx = x0 + ox;
-  if (gy >= H || gx >= W) return;
-  float b0 = 0.f, b1 = 0.f, b2 = 0.f;
-  for (int k = 0; k <= 2 * R; ++k) {
-    const float w = win.w[k];
-    b0 = __builtin_fmaf(w, sh[0][oy + k][ox], b0);
-    b1 = __builtin_fmaf(w, sh[1][oy + k][ox], b1);
-    b2 = __builtin_fmaf(w, sh[2][oy + k][ox], b2);
+  constexpr int kItems = (PH * kSegs + kThreads - 1) / kThreads;
+  f2 hs01[kItems][kSeg];
+  float hs2[kItems][kSeg];
+#pragma unroll
+  for (int it = 0; it < kItems; ++it) {  // horizontal pass
+    const int i = threadIdx.x + it * kThreads, r = i / kSegs, q0 = (i % kSegs) * kSeg;
+    if (i >= PH * kSegs) break;
+    f2 u01[kSeg + 2 * R];
+    float u2[kSeg + 2 * R];
+#pragma unroll
+    for (int j = 0; j < kSeg + 2 * R; ++j) {
+      u01[j] = sp[r][q0 + j];
+      u2[j] = s2[r][q0 + j];
+    }
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) {
+      f2 b01 = {0.f, 0.f};
+      float b2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        b01 = __builtin_elementwise_fma((f2){w[k], w[k]}, u01[o + k], b01);
+        b2 = __builtin_fmaf(w[k], u2[o + k], b2);
+      }
+      hs01[it][o] = b01;
+      hs2[it][o] = b2;
+    }
   }
-  const size_t o = c * plane + (size_t)gy * W + gx;
-  const float x = a.pred[o], y = a.target[o];
+  const int col = threadIdx.x % kTW, r0 = (threadIdx.x / kTW) * kRows, gx = x0 + col;
+  float xc[kRows], yc[kRows];  // this thread's output pixels, fetched while the row sums settle
+#pragma unroll
+  for (int o = 0; o < kRows; ++o) {
+    const int gy = y0 + r0 + o;
+    const bool in = gy < H && gx < W;
+    const size_t p = c * plane + (size_t)gy * W + gx;
+    xc[o] = in ? a.pred[p] : 0.f;
+    yc[o] = in ? a.target[p] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < kItems; ++it) {
+    const int i = threadIdx.x + it * kThreads, r = i / kSegs, q0 = (i % kSegs) * kSeg;
+    if (i >= PH * kSegs) break;
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) {
+      hp[r][q0 + o] = hs01[it][o];
+      h2[r][q0 + o] = hs2[it][o];
+    }
+  }
+  __syncthreads();
+  f2 a01[kRows];
+  float a2[kRows];
+#pragma unroll
+  for (int o = 0; o < kRows; ++o) {
+    a01[o] = (f2){0.f, 0.f};
+    a2[o] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < kRows + 2 * R; ++j) {
+    const f2 b01 = hp[r0 + j][col];
+    const float b2 = h2[r0 + j][col];
+#pragma unroll
+    for (int o = 0; o < kRows; ++o) {
+      const int k = j - o;
+      if (k >= 0 && k < K) {
+        a01[o] = __builtin_elementwise_fma((f2){w[k], w[k]}, b01, a01[o]);
+        a2[o] = __builtin_fmaf(w[k], b2, a2[o]);
+      }
+    }
+  }
   const float inv_n = 1.f / (float)n;
   const float gt = a.g_total ? *a.g_total : 1.f;
-  const float sgn = x > y ? 1.f : (x < y ? -1.f : 0.f);  // abs backward (sign, 0 at 0)
-  const float d_ssim = b0 + 2.f * x * b1 + y * b2;     // d(sum of clamped SSIM)/dx
-  a.d_pred[o] = gt * (((1.f - a.lambda_dssim) * inv_n) * sgn - (a.lambda_dssim * inv_n) * d_ssim);
+#pragma unroll
+  for (int o = 0; o < kRows; ++o) {
+    const int gy = y0 + r0 + o;
+    if (gy >= H || gx >= W) continue;
+    const size_t p = c * plane + (size_t)gy * W + gx;
+    const float x = xc[o], y = yc[o];
+    const float sgn = x > y ? 1.f : (x < y ? -1.f : 0.f);  // abs backward (sign, 0 at 0)
+    const float d_ssim = a01[o].x + 2.f * x * a01[o].y + y * a2[o];  // d(sum of clamped SSIM)/dx
+    a.d_pred[p] = gt * (((1.f - a.lambda_dssim) * inv_n) * sgn - (a.lambda_dssim * inv_n) * d_ssim);
+  }
 }
 
 bool window_of(int k, Window &win) {
@@ -197,28 +358,50 @@ bool window_of(int k, Window &win) {
   return true;
 }
 
-inline unsigned blocks_of(int v) { return (unsigned)((v + kT - 1) / kT); }
+inline unsigned blocks_of(int v, int t) { return (unsigned)((v + t - 1) / t); }
+
+inline dim3 grid_of(const gs_loss_args &a) {
+  return dim3(blocks_of(a.width, kTW), blocks_of(a.height, kTH), a.channels);
+}
+
+template <int R>
+void launch_fwd(const gs_loss_args &a, const Window &win, float2 *partials, hipStream_t s) {
+  k_loss_fwd<R><<<grid_of(a), kThreads, 0, s>>>(a, win, partials);
+}
+
+template <int R>
+void launch_bwd(const gs_loss_args &a, const Window &win, hipStream_t s) {
+  k_loss_bwd<R><<<grid_of(a), kThreads, 0, s>>>(a, win);
+}
+
+using FwdLaunch = void (*)(const gs_loss_args &, const Window &, float2 *, hipStream_t);
+using BwdLaunch = void (*)(const gs_loss_args &, const Window &, hipStream_t);
+static_assert(kMaxR == 5, "one instantiation per window radius 0..kMaxR");
+constexpr FwdLaunch kFwd[kMaxR + 1] = {launch_fwd<0>, launch_fwd<1>, launch_fwd<2>,
+                                       launch_fwd<3>, launch_fwd<4>, launch_fwd<5>};
+constexpr BwdLaunch kBwd[kMaxR + 1] = {launch_bwd<0>, launch_bwd<1>, launch_bwd<2>,
+                                       launch_bwd<3>, launch_bwd<4>, launch_bwd<5>};
 
 }  // namespace
 
 extern "C" size_t gs_loss_workspace_bytes(int32_t channels, int32_t height, int32_t width) {
   if (channels <= 0 || height <= 0 || width <= 0) return 0;
-  return sizeof(float2) * (size_t)blocks_of(width) * blocks_of(height) * channels;
+  return sizeof(float2) * (size_t)blocks_of(width, kTW) * blocks_of(height, kTH) * channels;
 }
 
 extern "C" gs_status gs_loss_forward(const gs_loss_args *a, gs_stream_t stream) {
   if (!a) return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_loss_forward");
   Window win;
   if (!window_of(a->window, win)) return gs_internal_fail(GS_ERR_UNSUPPORTED, "%s: window must be odd, 1..11", "gs_loss_forward");
-  if (a->channels <= 0 || a->height <= 0 || a->width <= 0 || a->height > 65535 * kT || a->channels > 65535)
+  if (a->channels <= 0 || a->height <= 0 || a->width <= 0 || a->height > 65535 * kTH || a->channels > 65535)
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: bad shape", "gs_loss_forward");
   if (!a->pred || !a->target || !a->out || !a->workspace ||
       a->workspace_bytes < gs_loss_workspace_bytes(a->channels, a->height, a->width))
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: null buffer or small workspace", "gs_loss_forward");
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(blocks_of(a->width), blocks_of(a->height), a->channels);
+  const dim3 grid = grid_of(*a);
   float2 *partials = (float2 *)a->workspace;
-  k_loss_fwd<<<grid, kThreads, 0, s>>>(*a, win, partials);
+  kFwd[win.r](*a, win, partials, s);
   k_loss_final<<<1, 1024, 0, s>>>(*a, partials, (int)(grid.x * grid.y * grid.z));
   return gs_internal_check_launch("gs_loss_forward");
 }
@@ -227,12 +410,11 @@ extern "C" gs_status gs_loss_backward(const gs_loss_args *a, gs_stream_t stream)
   if (!a) return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_loss_backward");
   Window win;
   if (!window_of(a->window, win)) return gs_internal_fail(GS_ERR_UNSUPPORTED, "%s: window must be odd, 1..11", "gs_loss_backward");
-  if (a->channels <= 0 || a->height <= 0 || a->width <= 0 || a->height > 65535 * kT || a->channels > 65535)
+  if (a->channels <= 0 || a->height <= 0 || a->width <= 0 || a->height > 65535 * kTH || a->channels > 65535)
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: bad shape", "gs_loss_backward");
   if (!a->pred || !a->target || !a->maps || !a->d_pred)
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_loss_backward");
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(blocks_of(a->width), blocks_of(a->height), a->channels);
-  k_loss_bwd<<<grid, kThreads, 0, s>>>(*a, win);
+  kBwd[win.r](*a, win, s);
   return gs_internal_check_launch("gs_loss_backward");
 }

@@ -894,6 +894,25 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
 // per round unless the round's rectangles average more than 64 tiles); then
 // every thread writes consecutive output entries, looking its Gaussian up in
 // one LDS read (a binary search over the offsets took 8 dependent ones).
+// Runs [lo, hi) longer than kWaveFillRun, flagged per lane by `wide`, are
+// written by the whole wave, one run after another, 64 positions per step:
+// fill(position, value of the lane that owns the run).  Every active lane of
+// the wave must call it (a ballot and shuffles inside, outside the divergent
+// fill loop); lanes with nothing to fill pass wide = false.
+constexpr uint32_t kWaveFillRun = 32;
+template <typename Fill>
+__device__ __forceinline__ void wave_fill_runs(bool wide, uint32_t lo, uint32_t hi, uint32_t value, Fill fill) {
+  unsigned long long m = __ballot(wide);
+  const uint32_t lane = threadIdx.x & 63u;
+  while (m) {
+    const int l = __ffsll(m) - 1;
+    m &= m - 1;
+    const uint32_t rlo = (uint32_t)__shfl((int)lo, l, 64), rhi = (uint32_t)__shfl((int)hi, l, 64);
+    const uint32_t v = (uint32_t)__shfl((int)value, l, 64);
+    for (uint32_t o = rlo + lane; o < rhi; o += 64) fill(o, v);
+  }
+}
+
 constexpr uint32_t kOwnerCap = kBlock * 64;
 __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials) {
   __shared__ uint32_t s_off[kBlock + 1];
@@ -941,7 +960,14 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
     for (uint32_t wb = 0; wb < tot; wb += kOwnerCap) {
       if (wb) __syncthreads();  // the previous window's owner reads are done
       const uint32_t lo_c = ex > wb ? ex : wb, hi_c = min(ex + cnt, wb + kOwnerCap);
-      for (uint32_t o = lo_c; o < hi_c; ++o) s_owner[o - wb] = (uint8_t)threadIdx.x;
+      // short runs by their own lane; a wide rectangle's run (up to a whole
+      // window) by its wave, 64 entries per step
+      const bool wide = hi_c > lo_c + kWaveFillRun;
+      if (!wide)
+        for (uint32_t o = lo_c; o < hi_c; ++o) s_owner[o - wb] = (uint8_t)threadIdx.x;
+      wave_fill_runs(wide, lo_c - wb, hi_c - wb, threadIdx.x, [&](uint32_t o, uint32_t owner) {
+        s_owner[o] = (uint8_t)owner;
+      });
       __syncthreads();
       const uint32_t wend = min(tot, wb + kOwnerCap);
       for (uint32_t o = wb + threadIdx.x; o < wend; o += kBlock) {
@@ -990,13 +1016,16 @@ __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
   }
   const long long prev = p > 0 ? (long long)a.sorted_keys[p - 1] : -1;
   const long long cur = p < a.num_pairs ? (long long)a.sorted_keys[p] : (long long)a.num_tiles;
-  if (cur == prev) return;
-  if (prev >= 0) a.ranges[2 * prev + 1] = (uint32_t)p;
-  for (long long t = prev + 1; t < cur; ++t) {
-    a.ranges[2 * t] = (uint32_t)p;
-    a.ranges[2 * t + 1] = (uint32_t)p;
-  }
-  if (cur < a.num_tiles) a.ranges[2 * cur] = (uint32_t)p;
+  const bool edge = cur != prev;
+  if (edge && prev >= 0) a.ranges[2 * prev + 1] = (uint32_t)p;
+  if (edge && cur < a.num_tiles) a.ranges[2 * cur] = (uint32_t)p;
+  // the empty tiles in between: a short gap by its lane, a long one (a sparse
+  // frame) by the wave, 64 tiles per step
+  const uint32_t t0 = (uint32_t)(prev + 1), t1 = edge ? (uint32_t)cur : t0;
+  const bool wide = t1 > t0 + kWaveFillRun;
+  if (!wide)
+    for (uint32_t t = t0; t < t1; ++t) a.ranges[2 * t] = a.ranges[2 * t + 1] = (uint32_t)p;
+  wave_fill_runs(wide, t0, t1, (uint32_t)p, [&](uint32_t t, uint32_t q) { a.ranges[2 * t] = a.ranges[2 * t + 1] = q; });
 }
 
 // ======================================================== blend fwd =======

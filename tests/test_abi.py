@@ -98,7 +98,7 @@ def test_loss_bad_arguments(pkg):
     assert lib.gs_loss_forward(C.byref(a), None) == 1  # null buffers
     assert b"gs_loss_forward" in lib.gs_last_error()
     assert lib.gs_loss_backward(C.byref(a), None) == 1
-    assert lib.gs_loss_workspace_bytes(3, 1080, 1920) == 8 * 3 * 68 * 120
+    assert lib.gs_loss_workspace_bytes(3, 1080, 1920) == 8 * 3 * 34 * 60  # one float2 per 32x32 tile
     assert lib.gs_loss_workspace_bytes(0, 4, 4) == 0
 
 

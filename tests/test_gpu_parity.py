@@ -564,6 +564,18 @@ def test_wide_rects_vs_oracle(pkg, cuda):
     assert not errs, errs
 
 
+def test_sparse_frame_vs_oracle(pkg, cuda):
+    """A few small Gaussians in a 640 x 480 frame of 4-px tiles (19,200
+    tiles): runs of thousands of empty tiles between the tile lists, written
+    by whole waves in k_tile_ranges."""
+    W, H = 640, 480
+    sc = pkg.synthetic.make_scene(6, W, H, seed=47, sigma_range=(0.004, 0.01))
+    errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.3, 0.1, 0.0), renderer_kw=dict(tile_size=4),
+                                    label="sparse")
+    assert bad.sum() <= 2
+    assert not errs, errs
+
+
 @pytest.mark.parametrize("wh", [(1, 1), (5, 3), (17, 1), (1, 33), (129, 65)])
 def test_odd_image_sizes_vs_oracle(pkg, cuda, wh):
     """Images of one pixel, one row, one column, and sizes just past a tile
