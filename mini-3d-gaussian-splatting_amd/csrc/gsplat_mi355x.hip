@@ -895,21 +895,26 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
 // every thread writes consecutive output entries, looking its Gaussian up in
 // one LDS read (a binary search over the offsets took 8 dependent ones).
 // Runs [lo, hi) longer than kWaveFillRun, flagged per lane by `wide`, are
-// written by the whole wave, one run after another, 64 positions per step:
+// written by the wave's active lanes together, one run after another:
 // fill(position, value of the lane that owns the run).  Every active lane of
-// the wave must call it (a ballot and shuffles inside, outside the divergent
-// fill loop); lanes with nothing to fill pass wide = false.
+// the wave must call it (ballots and shuffles inside, outside the divergent
+// fill loop); lanes with nothing to fill pass wide = false.  Lanes that have
+// already left the kernel (a partial last wave) take no part: the stride is
+// the number of active lanes, not 64.
 constexpr uint32_t kWaveFillRun = 32;
 template <typename Fill>
 __device__ __forceinline__ void wave_fill_runs(bool wide, uint32_t lo, uint32_t hi, uint32_t value, Fill fill) {
   unsigned long long m = __ballot(wide);
+  if (!m) return;
+  const unsigned long long act = __ballot(1);
   const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nact = (uint32_t)__popcll(act), rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
   while (m) {
     const int l = __ffsll(m) - 1;
     m &= m - 1;
     const uint32_t rlo = (uint32_t)__shfl((int)lo, l, 64), rhi = (uint32_t)__shfl((int)hi, l, 64);
     const uint32_t v = (uint32_t)__shfl((int)value, l, 64);
-    for (uint32_t o = rlo + lane; o < rhi; o += 64) fill(o, v);
+    for (uint32_t o = rlo + rank; o < rhi; o += nact) fill(o, v);
   }
 }
 
