@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 12
+#define GS_ABI_VERSION 13
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
@@ -330,7 +330,11 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
  * torch.optim.Adam semantics (amsgrad off, weight_decay 0):
  *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
  *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
- * Tensors with grad == NULL are skipped (torch skips params without grad). */
+ * Tensors with grad == NULL are skipped (torch skips params without grad).
+ * param_out: NULL updates p in place (torch's behaviour); otherwise p is
+ * only read and the updated parameter is written to param_out (same
+ * numel, no overlap with p) -- the same reads and writes as the in-place
+ * step, e.g. for a benchmark that renders one fixed scene every step. */
 #define GS_ADAM_MAX_TENSORS 8
 typedef struct gs_adam_tensor {
   float *param, *exp_avg, *exp_avg_sq;
@@ -339,6 +343,7 @@ typedef struct gs_adam_tensor {
   float lr;
   float bias_correction1; /* 1 - beta1^step */
   float bias_correction2_sqrt; /* sqrt(1 - beta2^step) */
+  float *param_out;       /* NULL: in place */
 } gs_adam_tensor;
 typedef struct gs_adam_args {
   int32_t num_tensors;

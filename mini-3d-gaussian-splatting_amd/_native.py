@@ -27,7 +27,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 12
+GS_ABI_VERSION = 13
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -111,6 +111,7 @@ class GsAdamTensor(C.Structure):
     _fields_ = [
         ("param", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("grad", _vp), ("numel", C.c_int64),
         ("lr", C.c_float), ("bias_correction1", C.c_float), ("bias_correction2_sqrt", C.c_float),
+        ("param_out", _vp),
     ]
 
 

@@ -2290,11 +2290,13 @@ __global__ __launch_bounds__(kBlock) void k_adam(gs_adam_args a, int4 firsts0, i
   for (int k = 1; k < GS_ADAM_MAX_TENSORS; ++k) ti += (int)blockIdx.x >= starts[k] ? 1 : 0;
   const gs_adam_tensor &t = a.t[ti];
   if (!t.grad) return;
+  float *const pout = t.param_out ? t.param_out : t.param;  // (in place unless an output is given)
   const int64_t base = (int64_t)(blockIdx.x - starts[ti]) * kAdamChunk;
   const float b1 = a.beta1, b2 = a.beta2, om1 = 1.f - b1, om2 = 1.f - b2;
   const float step = t.lr / t.bias_correction1, bc2s = t.bias_correction2_sqrt;
   const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
-                     reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
+                     reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq) |
+                     reinterpret_cast<uintptr_t>(pout)) & 15) == 0;
   if (vec && base + kAdamChunk <= t.numel) {
     // whole chunk in range (all but a tensor's last block): the four rounds'
     // loads issued together, no branch between them -- under the per-round
@@ -2317,7 +2319,7 @@ __global__ __launch_bounds__(kBlock) void k_adam(gs_adam_args a, int4 firsts0, i
       p[r].c -= step * (m[r].c / (sqrtf(v[r].c) / bc2s + a.eps));
       GS_ADAM_1(x) GS_ADAM_1(y) GS_ADAM_1(z) GS_ADAM_1(w)
 #undef GS_ADAM_1
-      *reinterpret_cast<float4 *>(t.param + i0) = p[r];
+      *reinterpret_cast<float4 *>(pout + i0) = p[r];
       *reinterpret_cast<float4 *>(t.exp_avg + i0) = m[r];
       *reinterpret_cast<float4 *>(t.exp_avg_sq + i0) = v[r];
     }
@@ -2337,7 +2339,7 @@ __global__ __launch_bounds__(kBlock) void k_adam(gs_adam_args a, int4 firsts0, i
       p.c -= step * (m.c / (sqrtf(v.c) / bc2s + a.eps));
       GS_ADAM_1(x) GS_ADAM_1(y) GS_ADAM_1(z) GS_ADAM_1(w)
 #undef GS_ADAM_1
-      *reinterpret_cast<float4 *>(t.param + i0) = p;
+      *reinterpret_cast<float4 *>(pout + i0) = p;
       *reinterpret_cast<float4 *>(t.exp_avg + i0) = m;
       *reinterpret_cast<float4 *>(t.exp_avg_sq + i0) = v;
     } else {
@@ -2347,7 +2349,7 @@ __global__ __launch_bounds__(kBlock) void k_adam(gs_adam_args a, int4 firsts0, i
         const float v = b2 * t.exp_avg_sq[i] + om2 * (g * g);
         t.exp_avg[i] = m;
         t.exp_avg_sq[i] = v;
-        t.param[i] -= step * (m / (sqrtf(v) / bc2s + a.eps));
+        pout[i] = t.param[i] - step * (m / (sqrtf(v) / bc2s + a.eps));
       }
     }
   }

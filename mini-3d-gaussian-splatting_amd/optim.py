@@ -19,6 +19,18 @@ from . import _native as N
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        # parameter -> tensor the updated value is written to instead of the
+        # parameter (gs_adam_tensor.param_out); empty: in place, as torch
+        self.param_out = {}
+
+    def set_output(self, param: torch.Tensor, out: torch.Tensor) -> None:
+        """Write param's updates to `out` (same shape, contiguous fp32, no
+        overlap) and leave param unchanged: the in-place step's reads and
+        writes, for a benchmark that renders one fixed scene every step."""
+        if out.shape != param.shape or out.dtype != torch.float32 or not out.is_contiguous() or \
+                out.device != param.device or out.data_ptr() == param.data_ptr():
+            raise ValueError("param_out must be a separate contiguous fp32 tensor shaped like the parameter")
+        self.param_out[param] = out
 
     def _begin(self):
         """Advance every parameter with a gradient by one step: the descriptors
@@ -42,7 +54,7 @@ class FusedAdam(torch.optim.Optimizer):
                 rows = p.shape[0] if p.dim() else 1
                 batches.setdefault((float(b1), float(b2), float(group["eps"])), []).append(
                     (p, st["exp_avg"], st["exp_avg_sq"], p.grad, rows, float(group["lr"]), 1.0 - b1 ** t,
-                     (1.0 - b2 ** t) ** 0.5))
+                     (1.0 - b2 ** t) ** 0.5, self.param_out.get(p)))
         return batches
 
     @staticmethod
@@ -56,7 +68,7 @@ class FusedAdam(torch.optim.Optimizer):
                 chunk = ds[i:i + N.GS_ADAM_MAX_TENSORS]
                 a = N.GsAdamArgs()
                 a.num_tensors, a.beta1, a.beta2, a.eps = len(chunk), b1, b2, eps
-                for k, (p, m, v, g, rows, lr, bc1, bc2s) in enumerate(chunk):
+                for k, (p, m, v, g, rows, lr, bc1, bc2s, out) in enumerate(chunk):
                     if lo is None:
                         off, num = 0, p.numel()
                     else:
@@ -64,7 +76,8 @@ class FusedAdam(torch.optim.Optimizer):
                         r0, r1 = min(lo, rows), min(hi, rows)
                         off, num = r0 * cols, (r1 - r0) * cols
                     a.t[k] = N.GsAdamTensor(N.ptr(p) + 4 * off, N.ptr(m) + 4 * off, N.ptr(v) + 4 * off,
-                                            N.ptr(g) + 4 * off, num, lr, bc1, bc2s)
+                                            N.ptr(g) + 4 * off, num, lr, bc1, bc2s,
+                                            N.ptr(out) + 4 * off if out is not None else None)
                 N.check(lib.gs_adam_step(C.byref(a), stream), "gs_adam_step")
 
     @torch.no_grad()

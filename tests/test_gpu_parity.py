@@ -412,6 +412,39 @@ def test_fused_adam_matches_torch_adam(pkg, cuda):
         assert torch.allclose(x, y, rtol=1e-5, atol=1e-5), (x - y).abs().max()  # fp32 rounding of two Adam kernels
 
 
+def test_fused_adam_param_out(pkg, cuda):
+    """gs_adam_tensor.param_out: the parameter is only read and the update
+    goes to the output tensor, bit-identical to the in-place step's value;
+    the moments advance as in place.  Three steps from the same parameters
+    against in-place FusedAdam steps whose parameters are put back each time."""
+    g = torch.Generator().manual_seed(5)
+    shapes = [(999, 3), (1000, 4), (17,)]
+    a = [torch.randn(s, generator=g).to(cuda).requires_grad_() for s in shapes]
+    b = [t.detach().clone().requires_grad_() for t in a]
+    p0 = [t.detach().clone() for t in a]
+    oa = pkg.optim.FusedAdam([{"params": [t], "lr": 1e-2 * (i + 1)} for i, t in enumerate(a)])
+    ob = pkg.optim.FusedAdam([{"params": [t], "lr": 1e-2 * (i + 1)} for i, t in enumerate(b)])
+    outs = [torch.full_like(t, float("nan")) for t in a]
+    for t, o in zip(a, outs):
+        oa.set_output(t, o)
+    for it in range(3):
+        for x, y, s in zip(a, b, shapes):
+            gr = torch.randn(s, generator=g).to(cuda)
+            x.grad, y.grad = gr.clone(), gr.clone()
+        oa.step()
+        ob.step()
+        for x, y, o, q in zip(a, b, outs, p0):
+            assert torch.equal(x.detach(), q)        # the parameter is untouched
+            assert torch.equal(o, y.detach())        # the update, bit for bit
+            with torch.no_grad():
+                y.copy_(q)                           # in-place reference back to the same start
+    for x, y in zip(a, b):
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(oa.state[x][k], ob.state[y][k])
+    with pytest.raises(ValueError):
+        oa.set_output(a[0], a[0])
+
+
 @pytest.mark.parametrize("bg", [(0.0, 0.0, 0.0), (0.3, 0.2, 0.1)])
 def test_long_tile_lists_vs_oracle(pkg, cuda, bg):
     """Tiles with > 256 entries (several forward batches, many backward
