@@ -71,9 +71,10 @@ def run(out_png: str | None = None, check: bool = True, verbose: bool = True) ->
     # 1. the reference's workflow: a random model, a posed camera, render + backward
     g = pkg.GaussianModel(pkg.TrainingConfig())
     g.create_from_random(5000, scene_extent=1.0, device=dev, generator=torch.Generator().manual_seed(0))
-    with torch.no_grad():
-        g._scaling.add_(torch.empty_like(g._scaling).uniform_(-0.5, 0.5))
-        g._opacity.normal_(0.0, 1.0)
+    with torch.no_grad():  # (seeded: the example prints the same numbers every run)
+        gen = torch.Generator().manual_seed(1)
+        g._scaling.add_((torch.rand(g._scaling.shape, generator=gen) - 0.5).to(dev))
+        g._opacity.copy_(torch.randn(g._opacity.shape, generator=gen).to(dev))
     cam = pkg.Camera(uid=0, R=np.eye(3, dtype=np.float32), T=np.array([0.0, 0.0, -3.0], np.float32),
                      FoVx=math.radians(60), FoVy=math.radians(60), image=None, image_name="c1",
                      width=W, height=H)  # camera centre 3 units behind the origin, looking down +z
@@ -87,7 +88,7 @@ def run(out_png: str | None = None, check: bool = True, verbose: bool = True) ->
         out = renderer.render(cam, g, settings)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 100.0
-    res = {"visible": int(out["visibility_filter"].sum()), "mean_alpha": float(out["alpha"].mean()),
+    res = {"visible": int(out["visibility_filter"].sum()), "mean_alpha": float(out["alpha"].detach().mean()),
            "render_ms": ms, "grad_xyz_finite": bool(torch.isfinite(g._xyz.grad).all())}
     if out_png:
         _write_png(out_png, out["image"].detach().clamp(0, 1).cpu().numpy())

@@ -202,6 +202,11 @@ typedef struct gs_bin_args {
   int64_t capacity;      /* entries tile_keys / pair_gauss hold.  gs_bin_emit does nothing
                             when T = counters[1] > capacity, so it may be queued before T is
                             read back (then emit again into buffers of >= T entries) */
+  uint32_t *host_counters; /* optional: the device address of pinned host memory
+                              (hipHostGetDevicePointer) that gs_bin_count also writes
+                              counters[0..3] to, followed by a system-scope fence -- the
+                              caller reads (M, T) there after an event on the stream, with no
+                              copy in the stream.  NULL: counters only */
 } gs_bin_args;
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream);
 gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream);

@@ -65,7 +65,7 @@ class GsBinArgs(C.Structure):
         ("rects", _vp), ("vis", _vp), ("counters", _vp), ("key_minmax", _vp), ("workspace", _vp),
         ("workspace_bytes", C.c_size_t),
         ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp), ("records", _vp),
-        ("capacity", C.c_int64),
+        ("capacity", C.c_int64), ("host_counters", _vp),
     ]
 
 
@@ -236,3 +236,24 @@ def check(status: int, what: str):
 
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+_HIP = None
+
+
+def host_device_pointer(host: "torch.Tensor"):
+    """The device address of a pinned host tensor (hipHostGetDevicePointer on
+    the HIP runtime torch loaded), or None if the runtime does not map it --
+    the caller then copies through the stream instead."""
+    global _HIP
+    if not host.is_pinned():
+        return None
+    if _HIP is None:
+        tl = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        _HIP = C.CDLL(tl if os.path.exists(tl) else "libamdhip64.so.7")
+        _HIP.hipHostGetDevicePointer.argtypes = [C.POINTER(_vp), _vp, C.c_uint]
+        _HIP.hipHostGetDevicePointer.restype = C.c_int
+    d = _vp()
+    if _HIP.hipHostGetDevicePointer(C.byref(d), _vp(host.data_ptr()), 0) != 0 or not d.value:
+        return None
+    return int(d.value)

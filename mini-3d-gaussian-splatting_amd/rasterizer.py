@@ -371,6 +371,15 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         ba = N.GsBinArgs(n, cam.tiles_x, cam.tiles_y, N.ptr(sorted_ids), N.ptr(rects), N.ptr(vis),
                          N.ptr(counters), N.ptr(key_minmax), N.ptr(bws), bws.numel(), 0, 0, N.ptr(pair_offset),
                          N.ptr(records), 0)
+        per_thread = getattr(_HOST_COUNTERS, "bufs", None)
+        if per_thread is None:
+            per_thread = _HOST_COUNTERS.bufs = {}
+        hb = per_thread.get(dev)
+        if hb is None:
+            h = torch.empty((4,), dtype=i32, pin_memory=True)
+            hb = per_thread[dev] = (h, N.host_device_pointer(h))
+        host, host_dptr = hb
+        ba.host_counters = host_dptr
         StageTimer.mark("bin_count")
         N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
         # everything whose size does not depend on T is allocated before the
@@ -388,15 +397,12 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         # read-back's round trip.  T above the guess: re-allocate, re-emit.
         cap = _T_SEEN.get(dev, 0)
         big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, cam, dev) if cap else None
-        # (M, T) read back through pinned memory, copied BEFORE the emission
-        # is queued, so the host wakes while the GPU still emits
-        per_thread = getattr(_HOST_COUNTERS, "bufs", None)
-        if per_thread is None:
-            per_thread = _HOST_COUNTERS.bufs = {}
-        host = per_thread.get(dev)
-        if host is None:
-            host = per_thread[dev] = torch.empty((4,), dtype=i32, pin_memory=True)
-        host.copy_(counters[:4], non_blocking=True)
+        # (M, T) reach the host through pinned memory before the emission is
+        # queued, so the host wakes while the GPU still emits: gs_bin_count
+        # writes them there itself (host_counters, set up below) -- or, where
+        # the runtime does not map the buffer, a copy in the stream
+        if host_dptr is None:
+            host.copy_(counters[:4], non_blocking=True)
         ready = torch.cuda.Event()
         ready.record()
         if big_guess is not None:
