@@ -202,11 +202,13 @@ typedef struct gs_bin_args {
   int64_t capacity;      /* entries tile_keys / pair_gauss hold.  gs_bin_emit does nothing
                             when T = counters[1] > capacity, so it may be queued before T is
                             read back (then emit again into buffers of >= T entries) */
-  uint32_t *host_counters; /* optional: the device address of pinned host memory
+  uint32_t *host_counters; /* optional [5]: the device address of pinned host memory
                               (hipHostGetDevicePointer) that gs_bin_count also writes
-                              counters[0..3] to, followed by a system-scope fence -- the
-                              caller reads (M, T) there after an event on the stream, with no
-                              copy in the stream.  NULL: counters only */
+                              counters[0..3] to, then -- after a system-scope fence --
+                              host_seq to [4]: the caller polls [4] for the value it passed
+                              and reads (M, T) with no copy and no event in the stream.
+                              NULL: counters only */
+  uint32_t host_seq;
 } gs_bin_args;
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream);
 gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream);

@@ -65,7 +65,7 @@ class GsBinArgs(C.Structure):
         ("rects", _vp), ("vis", _vp), ("counters", _vp), ("key_minmax", _vp), ("workspace", _vp),
         ("workspace_bytes", C.c_size_t),
         ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp), ("records", _vp),
-        ("capacity", C.c_int64), ("host_counters", _vp),
+        ("capacity", C.c_int64), ("host_counters", _vp), ("host_seq", C.c_uint32),
     ]
 
 

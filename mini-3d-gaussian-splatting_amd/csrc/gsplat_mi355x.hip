@@ -831,7 +831,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
 // exclusive scan of the touch partials (single block); counters[0] = M, [1] = T,
 // [2] / [3] = min / max visible depth bits (the projection's per-block values)
 __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials, int nb, uint32_t *counters,
-                                                               uint32_t *host_counters) {
+                                                               uint32_t *host_counters, uint32_t host_seq) {
   __shared__ uint32_t s_tmp[4];
   __shared__ uint32_t s_mm[2][kBlock / kWave];
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
@@ -891,6 +891,8 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
       host_counters[1] = carry;
       host_counters[2] = mn;
       host_counters[3] = mx;
+      __threadfence_system();  // the counters reach the host before the sequence word
+      host_counters[4] = host_seq;
       __threadfence_system();
     }
   }
@@ -2517,7 +2519,7 @@ gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
   const int nb = (int)div_up(a->n, kBinChunk);
   uint32_t *partials = (uint32_t *)a->workspace;
   k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials, nb);
-  k_bin_scan_partials<<<1, kBlock, 0, s>>>(partials, nb, a->counters, a->host_counters);
+  k_bin_scan_partials<<<1, kBlock, 0, s>>>(partials, nb, a->counters, a->host_counters, a->host_seq);
   return check_launch("gs_bin_count");
 }
 

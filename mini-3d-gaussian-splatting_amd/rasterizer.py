@@ -20,6 +20,7 @@ import ctypes as C
 import math
 import os
 import threading
+import time
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -171,6 +172,46 @@ _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess
 # read-back (renders from several threads each read their own counters; the
 # two per-device guesses above are only guesses, a stale one is corrected)
 _HOST_COUNTERS = threading.local()
+
+
+class _HostCounters:
+    """Pinned int32[8] gs_bin_count writes (M, T, depth-bits min / max) and
+    then a sequence word into, through its device address: the host polls the
+    word -- no copy and no event in the stream (an event record between the
+    count and the emission cost a ~6 us gap on the GPU).  Without a device
+    address (dptr None) the counters are copied and an event is waited for."""
+    __slots__ = ("t", "np", "dptr", "seq")
+
+    def __init__(self):
+        self.t = torch.empty((8,), dtype=torch.int32, pin_memory=True)
+        self.np = self.t.numpy()
+        self.dptr = N.host_device_pointer(self.t)
+        self.seq = 0
+
+    def arm(self, ba) -> None:
+        if self.dptr is None:
+            return
+        self.seq = self.seq % 0x7FFFFFFF + 1
+        self.np[4] = 0  # (the previous frame's word; the GPU writes this frame's after its counters)
+        ba.host_counters, ba.host_seq = self.dptr, self.seq
+
+    def wait(self, dev, ready) -> Tuple[int, int, int, int]:
+        if self.dptr is None:
+            ready.synchronize()
+        else:
+            hv, seq, i = self.np, self.seq, 0
+            deadline = time.perf_counter() + 10.0
+            while hv[4] != seq:
+                i += 1
+                if (i & 255) == 0:
+                    if time.perf_counter() > deadline:  # (never in a healthy run)
+                        torch.cuda.synchronize(dev)
+                        if hv[4] != seq:
+                            raise RuntimeError("gs_bin_count: the frame's counters never reached the host")
+                        break
+                    time.sleep(0)  # other host threads get the interpreter
+        v = self.np[:4].tolist()
+        return int(v[0]), int(v[1]), int(v[2]) & 0xFFFFFFFF, int(v[3]) & 0xFFFFFFFF
 _FUSE_FLAGS = os.environ.get("GS_FUSE_SLOT_FLAGS", "1") != "0"  # slot flags zeroed by gs_tile_ranges
 # Depth-key windows (per process and device; these are guesses, a stale one
 # only costs a re-render, so host threads may race on them): the window
@@ -374,12 +415,10 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         per_thread = getattr(_HOST_COUNTERS, "bufs", None)
         if per_thread is None:
             per_thread = _HOST_COUNTERS.bufs = {}
-        hb = per_thread.get(dev)
-        if hb is None:
-            h = torch.empty((4,), dtype=i32, pin_memory=True)
-            hb = per_thread[dev] = (h, N.host_device_pointer(h))
-        host, host_dptr = hb
-        ba.host_counters = host_dptr
+        hc = per_thread.get(dev)
+        if hc is None:
+            hc = per_thread[dev] = _HostCounters()
+        hc.arm(ba)
         StageTimer.mark("bin_count")
         N.check(lib.gs_bin_count(C.byref(ba), s), "gs_bin_count")
         # everything whose size does not depend on T is allocated before the
@@ -399,12 +438,13 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         big_guess = _alloc_tile_buffers(lib, cap + cap // 4 + 4096, num_tiles, cam, dev) if cap else None
         # (M, T) reach the host through pinned memory before the emission is
         # queued, so the host wakes while the GPU still emits: gs_bin_count
-        # writes them there itself (host_counters, set up below) -- or, where
-        # the runtime does not map the buffer, a copy in the stream
-        if host_dptr is None:
-            host.copy_(counters[:4], non_blocking=True)
-        ready = torch.cuda.Event()
-        ready.record()
+        # writes them there itself (_HostCounters) -- or, where the runtime
+        # does not map the buffer, a copy in the stream and an event
+        ready = None
+        if hc.dptr is None:
+            hc.t[:4].copy_(counters[:4], non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record()
         if big_guess is not None:
             gb, gcap = big_guess[0].data_ptr(), big_guess[1]
             ba.tile_keys, ba.pair_gauss, ba.capacity = gb, gb + 8 * gcap, gcap
@@ -414,8 +454,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
             # (the GPU is emitting): after the sync only T is filled in
             layout = _tile_layout(lib, big_guess, num_tiles, cam)
         StageTimer.mark("~sync")
-        ready.synchronize()  # the one host sync
-        M, T, zmin, zmax = (int(v) & 0xFFFFFFFF if i >= 2 else int(v) for i, v in enumerate(host.tolist()))
+        M, T, zmin, zmax = hc.wait(dev, ready)  # the one host sync
         if not window_holds(window, zmin, zmax):
             # a visible depth outside the window (the sort's keys were clipped),
             # or an MSD bucket over capacity (the depth max poisoned)
