@@ -842,6 +842,41 @@ def test_float64_inputs_cast(pkg, cuda):
         pkg.GaussianRenderer().render(cam, g_bad, st)
 
 
+def test_counters_polled_and_copied_agree(pkg, cuda):
+    """(M, T) reach the host either written by gs_bin_count into the pinned
+    buffer through its device address and polled (the default), or copied in
+    the stream behind an event (where the runtime does not map the buffer):
+    both give the same frame, including a frame whose T exceeds the previous
+    frame's capacity guess (a re-emission)."""
+    from mini3dgs_amd import rasterizer as RZ
+    syn = pkg.synthetic
+    W, H = 256, 192
+    small, big = (syn.make_scene(n, W, H, seed=90 + n % 7) for n in (2000, 30000))
+    st = pkg.RenderSettings(H, W, torch.tensor([0.0, 0.1, 0.2]))
+
+    def frames():
+        out = []
+        for sc in (small, big, small):
+            m = syn.to_model(sc, pkg.GaussianModel, cuda)
+            with torch.no_grad():
+                o = pkg.GaussianRenderer().render(Cam(W, H, sc.fovx, sc.fovy), m, st)
+            out.append((o["image"].clone(), o["alpha"].clone()))
+        return out
+
+    polled = frames()
+    hc = RZ._HOST_COUNTERS.bufs[cuda]
+    assert hc.dptr is not None  # the runtime maps pinned memory on this image
+    saved = hc.dptr
+    try:
+        hc.dptr = None
+        RZ._T_SEEN.pop(cuda, None)
+        copied = frames()
+    finally:
+        hc.dptr = saved
+    for (a, b), (c, d) in zip(polled, copied):
+        assert torch.equal(a, c) and torch.equal(b, d)
+
+
 def test_concurrent_renders_two_threads(pkg, cuda):
     """SURVEY 8(b) threading row: renders from two host threads on their own
     streams, concurrently, give each thread's frames exactly as a lone render
