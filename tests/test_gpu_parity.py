@@ -842,6 +842,72 @@ def test_float64_inputs_cast(pkg, cuda):
         pkg.GaussianRenderer().render(cam, g_bad, st)
 
 
+@pytest.mark.parametrize("n,w,h,tile", [(20000, 320, 240, 16), (100000, 800, 800, 16), (6000, 200, 152, 8),
+                                         (1000000, 1920, 1080, 16)])
+def test_index_work_bit_exact(pkg, cuda, n, w, h, tile):
+    """The integer and index stages bit-exact: the visible set and
+    count M, the depth order (ascending z, ties by Gaussian index -- a stable
+    sort of the frame's own depths), each visible Gaussian's tile rectangle by
+    the reference's int() rule (renderer.py:278-293), and every tile's list
+    (renderer.py:294-298: Gaussians in depth order) with its [start, end)
+    range, T entries in all.  The GPU's own projections are the inputs, so no
+    rounding enters; M, T and the depth order are also equal to the oracle's
+    on these scenes."""
+    from mini3dgs_amd import rasterizer as RZ
+    sc = pkg.synthetic.make_scene(n, w, h, seed=n % 97)
+    m = pkg.synthetic.to_model(sc, pkg.GaussianModel, cuda)
+    cam = pkg.camera_params(Cam(w, h, sc.fovx, sc.fovy), pkg.RenderSettings(h, w, torch.zeros(3)), tile_size=tile)
+    with torch.no_grad():
+        _, _, _, means2d, _, radii, vis, fr = RZ.forward_pipeline(
+            cam, m._xyz, None, m._scaling, m._rotation, m._features_dc[:, 0, :],
+            torch.sigmoid(m._opacity).squeeze(1))
+    torch.cuda.synchronize()
+    M, T = fr.M, fr.T
+    vis = vis.cpu().numpy().astype(bool)
+    z = fr.records.view(-1, 12)[:, 9].cpu().numpy()
+    order = fr.order.cpu().numpy()[:M].astype(np.int64)
+    vidx = np.nonzero(vis)[0]
+    assert M == len(vidx)
+    want_order = vidx[np.argsort(z[vidx], kind="stable")]
+    assert np.array_equal(order, want_order)
+    # rectangles: renderer.py:278-293 from this frame's means and radii
+    mx, my = means2d.cpu().numpy().T.astype(np.float32)
+    ri = np.trunc(radii.cpu().numpy()).astype(np.int64)
+    icx, icy = np.trunc(mx).astype(np.int64), np.trunc(my).astype(np.int64)
+    x0, x1 = np.maximum(icx - ri, 0), np.minimum(icx + 1 + ri, w)
+    y0, y1 = np.maximum(icy - ri, 0), np.minimum(icy + 1 + ri, h)
+    rects = fr.rects.view(-1, 2).cpu().numpy().astype(np.int64)
+    gx0, gx1, gy0, gy1 = rects[:, 0] & 0xFFFF, rects[:, 0] >> 16, rects[:, 1] & 0xFFFF, rects[:, 1] >> 16
+    ne = (x0 < x1) & (y0 < y1)
+    v = vidx[ne[vidx]]
+    assert np.array_equal(gx0[v], x0[v] // tile) and np.array_equal(gx1[v], (x1[v] - 1) // tile)
+    assert np.array_equal(gy0[v], y0[v] // tile) and np.array_equal(gy1[v], (y1[v] - 1) // tile)
+    # tile lists: every (tile, Gaussian) of the depth-ordered rectangles, stable by tile
+    tiles_x, tiles_y = (w + tile - 1) // tile, (h + tile - 1) // tile
+    og = order[ne[order]]
+    nx = (x1[og] - 1) // tile - x0[og] // tile + 1
+    kk = nx * ((y1[og] - 1) // tile - y0[og] // tile + 1)
+    gs = np.repeat(og, kk)
+    local = np.arange(int(kk.sum())) - np.repeat(np.cumsum(kk) - kk, kk)  # rank in the rectangle, row-major
+    nxr = np.repeat(nx, kk)
+    keys = (np.repeat(y0[og] // tile, kk) + local // nxr) * tiles_x + np.repeat(x0[og] // tile, kk) + local % nxr
+    srt = np.argsort(keys, kind="stable")
+    assert T == len(keys)
+    assert np.array_equal(fr.sorted_gauss[:T].cpu().numpy().astype(np.int64), gs[srt])
+    counts = np.bincount(keys, minlength=tiles_x * tiles_y)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    rng_ = fr.ranges.cpu().numpy().astype(np.int64)
+    nz = counts > 0
+    assert np.array_equal(rng_[nz, 0], starts[nz]) and np.array_equal(rng_[nz, 1], (starts + counts)[nz])
+    assert np.all(rng_[~nz, 0] == rng_[~nz, 1])
+    # and the oracle's count and order on the same scene
+    if tile == 16:
+        cov = G.oracle().covariance(sc.scaling.numpy(), sc.rotation.numpy())
+        ref = G.oracle().render_forward(_oracle_scene(sc, cov, (0.0, 0.0, 0.0)), nthreads=8)
+        assert ref["M"] == M and ref["T"] == T
+        assert np.array_equal(ref["sorted_idx"].astype(np.int64), order)
+
+
 def test_counters_polled_and_copied_agree(pkg, cuda):
     """(M, T) reach the host either written by gs_bin_count into the pinned
     buffer through its device address and polled (the default), or copied in
