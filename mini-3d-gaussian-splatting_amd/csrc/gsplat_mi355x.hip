@@ -1081,6 +1081,9 @@ __device__ __forceinline__ float2 lds_pair(const float2 *p) {
 // s: |s_fp32 - s| <= ~4u (q00 dx^2 + |qo dx dy| + q11 dy^2) <= 4u (tr + |qo|)
 // tr / det * s, so conics with (tr + |qo|) tr > 1e4 det -- and
 // non-positive-definite or NaN ones -- are never culled.
+#ifndef GS_CELL_EXACT
+#define GS_CELL_EXACT 1
+#endif
 __device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo, float q11, float x0, float y0) {
   const float q01 = 0.5f * qo;
   const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
@@ -1089,7 +1092,28 @@ __device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo
   // v_rcp / v_sqrt (~1 ulp): far inside the 1% margin
   const float id = __builtin_amdgcn_rcpf(det);
   const float hx = __builtin_amdgcn_sqrtf(L * q11 * id), hy = __builtin_amdgcn_sqrtf(L * q00 * id);
-  return mx + hx >= x0 && mx - hx <= x0 + 7.f && my + hy >= y0 && my - hy <= y0 + 7.f;
+  const bool box = mx + hx >= x0 && mx - hx <= x0 + 7.f && my + hy >= y0 && my - hy <= y0 + 7.f;
+#if GS_CELL_EXACT
+  if (!box) return false;
+  // The ellipse's bounding box meets the cell: the minimum of s over the
+  // cell's box decides (a tilted, elongated ellipse's bounding box is much
+  // larger than it).  The mean inside the box: s = 0.  Otherwise the minimum
+  // lies on an edge: per edge the 1-D minimiser of the quadratic, clamped to
+  // the edge.  A point of the box is evaluated, so the fp32 value is s at a
+  // feasible point up to rounding -- the same ~4u (tr + |qo|) tr / det
+  // relative error as above, inside the 1% margin.
+  const float ax0 = x0 - mx, ax1 = x0 + 7.f - mx, ay0 = y0 - my, ay1 = y0 + 7.f - my;
+  if (ax0 <= 0.f && ax1 >= 0.f && ay0 <= 0.f && ay1 >= 0.f) return true;
+  const float kx = -0.5f * qo * __builtin_amdgcn_rcpf(q11), ky = -0.5f * qo * __builtin_amdgcn_rcpf(q00);
+  auto sv = [&](float dx, float dy) { return (dx * dx) * q00 + (qo * dx) * dy + (dy * dy) * q11; };
+  const float e0 = sv(ax0, __builtin_amdgcn_fmed3f(kx * ax0, ay0, ay1));
+  const float e1 = sv(ax1, __builtin_amdgcn_fmed3f(kx * ax1, ay0, ay1));
+  const float e2 = sv(__builtin_amdgcn_fmed3f(ky * ay0, ax0, ax1), ay0);
+  const float e3 = sv(__builtin_amdgcn_fmed3f(ky * ay1, ax0, ax1), ay1);
+  return fminf(fminf(e0, e1), fminf(e2, e3)) <= L;
+#else
+  return box;
+#endif
 }
 
 // Workgroup b -> (tile, cell): b, b+8, b+16, ... share an XCD (round-robin
