@@ -63,6 +63,33 @@ gs_status check_launch(const char *what) {
 
 inline unsigned div_up(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
+// Measurement-only (a variant build with -DGS_WAVE_TIMES, tools/wave_times.py):
+// each blend workgroup records its start and end on the 100 MHz real-time
+// clock and the XCD / CU it ran on, so the launch's occupancy over time and
+// its tail can be read back.  Not in the product build.
+#ifdef GS_WAVE_TIMES
+constexpr uint32_t kWtMax = 1u << 17;
+__device__ unsigned long long g_wave_times[2][kWtMax][3];
+struct WaveTimer {
+  int k;
+  unsigned long long t0;
+  __device__ explicit WaveTimer(int kk) : k(kk), t0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ ~WaveTimer() {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x < kWtMax) {
+      const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+      const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+      g_wave_times[k][blockIdx.x][0] = t0;
+      g_wave_times[k][blockIdx.x][1] = t1;
+      g_wave_times[k][blockIdx.x][2] = ((unsigned long long)xcc << 32) | hw;
+    }
+  }
+};
+#define GS_WAVE_TIMER(k) WaveTimer wave_timer_(k)
+#else
+#define GS_WAVE_TIMER(k)
+#endif
+
 // torch.clamp semantics (NaN propagates)
 __device__ __forceinline__ float clamp01(float v) { return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
 // clamp to [0,1] as the VALU clamp output modifier (folds into the producing
@@ -1116,14 +1143,32 @@ __device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo
 #endif
 }
 
-// Workgroup b -> (tile, cell): b, b+8, b+16, ... share an XCD (round-robin
-// dispatch; placement is for speed only), so the Q cells of a tile read its
-// records through one L2.  Grid: ceil(tiles / 8) * 8 Q.
-__device__ __forceinline__ void cell_tile(uint32_t b, int ncell, int &tile, int &quad) {
+// Workgroup b -> (tile, cell) and the tile's list range: b, b+8, b+16, ...
+// share an XCD (round-robin dispatch; placement is for speed only), so the Q
+// cells of a tile read its records through one L2.  Grid: ceil(tiles / 8) *
+// 8 Q.  Position (b / 8 / Q) * 8 + b % 8 is the tile itself, or, with a
+// dispatch order (gs_tile_order: the tiles with the most work first, so the
+// launch's last round is made of short workgroups), its entry (tile, start,
+// end) -- one load either way.  tile >= num_tiles: padding, no range.
+__device__ __forceinline__ void cell_tile(uint32_t b, int ncell, const uint32_t *order, const uint32_t *ranges,
+                                          int ntiles, int &tile, int &quad, uint32_t &start, uint32_t &end) {
   const uint32_t grp = b >> 3;
   const uint32_t q = (uint32_t)ncell;
   quad = (int)(grp % q);
-  tile = (int)((grp / q) * 8u + (b & 7u));
+  const uint32_t pos = (grp / q) * 8u + (b & 7u);
+  start = end = 0u;
+  if (order) {
+    const uint4 o = reinterpret_cast<const uint4 *>(order)[pos];
+    tile = (int)__builtin_amdgcn_readfirstlane(o.x);
+    start = __builtin_amdgcn_readfirstlane(o.y);
+    end = __builtin_amdgcn_readfirstlane(o.z);
+  } else {
+    tile = (int)pos;
+    if (tile < ntiles) {
+      start = __builtin_amdgcn_readfirstlane(ranges[2 * pos]);
+      end = __builtin_amdgcn_readfirstlane(ranges[2 * pos + 1]);
+    }
+  }
 }
 
 // Forward blend, one 64-lane workgroup per (tile, 8x8 cell), lane = pixel
@@ -1148,11 +1193,13 @@ __device__ __forceinline__ void cell_tile(uint32_t b, int ncell, int &tile, int 
 // constants).
 template <bool kCount, bool kT16>
 __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
+  GS_WAVE_TIMER(0);
   __shared__ float2 s_rec[kWave * 6];
   const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
   const int ncell = cg.cells();
   int tile, quad;
-  cell_tile(blockIdx.x, ncell, tile, quad);
+  uint32_t start, end;
+  cell_tile(blockIdx.x, ncell, a.tile_order, a.ranges, a.tiles_x * a.tiles_y, tile, quad, start, end);
   if (tile >= a.tiles_x * a.tiles_y) return;
   const int lane = threadIdx.x;
   const int cx0 = (quad % cg.QX) * 8, cy0 = (quad / cg.QX) * 8;  // the cell in its tile
@@ -1160,8 +1207,6 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
   const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
   const int W = a.cam.image_width, H = a.cam.image_height;
   const bool inside = cx0 + (lane & 7) < cg.L && cy0 + (lane >> 3) < cg.L && px < W && py < H;
-  const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]),
-                 end = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
   float ar = bg0, ag = bg1, ab = bg2;  // out_rgb = bg (renderer.py:273)
   // a lane is done once A >= kAlphaStop (the :352 break); lanes outside the
@@ -1173,6 +1218,7 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
   // evaluated entry (scalar), copied into a lane's neval only when it stops
   // (its bit leaves the running mask) -- two VALU less per evaluated entry
   uint32_t last = 0;
+  uint32_t work = 0;  // live (entry, cell) pairs: the backward's replay count
   unsigned long long runm = __builtin_amdgcn_ballot_w64(A < kAlphaStop);
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
@@ -1242,7 +1288,10 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
     }
     const uint64_t wi = (b - start) / 64u;
     if (lane == 0 && wi < live_left) live[wi] = livem;
+    work += (uint32_t)__builtin_popcountll(livem);
   }
+  // the entries the backward will replay in this cell: its dispatch-order key
+  if (a.cell_work && lane == 0) a.cell_work[(size_t)tile * ncell + quad] = work;
   if (!inside) return;
   if ((runm >> lane) & 1ull) neval = last;
   if (A < kAlphaStop) neval = end - start;
@@ -1256,6 +1305,124 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
   reinterpret_cast<float4 *>(a.pix_acc)[p] = make_float4(ar, ag, ab, D);
   reinterpret_cast<float2 *>(a.pix_state)[p] = make_float2(A, __uint_as_float(neval));
   if constexpr (kCount) a.pair_counts[p] = ncontrib;
+}
+
+// ================================================ blend dispatch order ====
+// The blend launches run ~4 rounds of workgroups per slot at C3, so the
+// launch ends with a round in which slots fall idle one by one; the longer
+// the workgroups still starting late, the longer that tail (measured with
+// per-workgroup clocks, tools/wave_times.py: residency averages 0.80 / 0.83
+// of its peak over the forward / backward launch).  k_tile_order lists the
+// tiles by expected work, largest first (a counting sort on 256 buckets of
+// key * 256 / (max + 1)), so the late starters are the short ones: the key is
+// the tile's list length before the forward, and the forward's per-cell
+// replay counts (cell_work, summed over the tile's cells) before the
+// backward.  Position p of the order is (tile, start, end, 0): the blend
+// workgroup reads its tile and list range in one load, as it read the range
+// before.  Only the dispatch order changes: every workgroup computes the same
+// outputs, so the order within a bucket (LDS atomics) is free.  Positions
+// past num_tiles (the grid's padding to 8) get tile = num_tiles, which the
+// blend kernels skip.  One 1024-thread workgroup; each thread holds 8 tiles'
+// keys (loads issued together) when num_tiles <= 8192, else re-reads them per
+// pass and chunk.
+constexpr int kOrdThreads = 1024, kOrdIpt = 8, kOrdChunk = kOrdThreads * kOrdIpt, kOrdBuckets = 256;
+// KIND 0: key = list length; 1: cell_work of 4 cells; 2: cell_work, any cells
+// (compile-time, so a thread's loads are issued together: under a runtime
+// branch each was waited for at its join, 16 us per launch)
+template <int KIND>
+__global__ __launch_bounds__(kOrdThreads) void k_tile_order(gs_order_args a) {
+  __shared__ uint32_t s_hist[kOrdBuckets];
+  __shared__ uint32_t s_max;
+  const int n = a.num_tiles, tid = threadIdx.x;
+  const int chunks = (n + kOrdChunk - 1) / kOrdChunk;
+  uint32_t key[kOrdIpt];
+  uint2 rg[kOrdIpt];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < kOrdIpt; ++j) {
+      const int t = c * kOrdChunk + j * kOrdThreads + tid;
+      const int tt = t < n ? t : 0;
+      rg[j] = reinterpret_cast<const uint2 *>(a.ranges)[tt];
+      uint32_t k;
+      if constexpr (KIND == 0) {
+        k = rg[j].y - rg[j].x;
+      } else if constexpr (KIND == 1) {
+        const uint4 w = reinterpret_cast<const uint4 *>(a.cell_work)[tt];
+        k = (w.x + w.y) + (w.z + w.w);
+      } else {
+        k = 0;
+        for (int q = 0; q < a.cells; ++q) k += a.cell_work[(size_t)tt * a.cells + q];
+      }
+      key[j] = t < n ? k : 0u;
+    }
+  };
+  if (tid == 0) s_max = 0;
+  if (tid < kOrdBuckets) s_hist[tid] = 0;
+  if (chunks == 1) load(0);
+  uint32_t m = 0;
+  for (int c = 0; c < chunks; ++c) {
+    if (chunks > 1) load(c);
+#pragma unroll
+    for (int j = 0; j < kOrdIpt; ++j) m = max(m, key[j]);
+  }
+  m = wave_max_u32(m);
+  __syncthreads();
+  if ((tid & (kWave - 1)) == 0) atomicMax(&s_max, m);
+  __syncthreads();
+  // (a float scale, not an integer division: a 64-bit divide is a long
+  // software sequence per key; any monotone bucket function will do)
+  const float scale = (float)kOrdBuckets / ((float)s_max + 1.f);
+  auto bucket = [&](uint32_t k) {
+    return (uint32_t)(kOrdBuckets - 1) - min((uint32_t)(kOrdBuckets - 1), (uint32_t)((float)k * scale));
+  };
+  // LDS atomics aggregated per wave: the lanes holding one bucket (ballot
+  // match) add once -- keys cluster in a few buckets, and same-address lanes
+  // of one atomic instruction serialise (11 us per launch unaggregated)
+  const unsigned long long lt = lanemask_lt();
+  for (int c = 0; c < chunks; ++c) {
+    if (chunks > 1) load(c);
+#pragma unroll
+    for (int j = 0; j < kOrdIpt; ++j) {
+      const bool valid = c * kOrdChunk + j * kOrdThreads + tid < n;
+      const uint32_t bk = bucket(key[j]);
+      const unsigned long long peers = match_digit(bk, 8, __ballot(valid));
+      if (valid && (peers & lt) == 0) atomicAdd(&s_hist[bk], (uint32_t)__popcll(peers));
+    }
+  }
+  __syncthreads();
+  if (tid < kWave) {  // exclusive scan of the 256 bucket counts: 4 per lane
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[i] = s_hist[4 * tid + i]; sum += v[i]; }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t t = __shfl_up(incl, d, kWave);
+      if (tid >= d) incl += t;
+    }
+    uint32_t run = incl - sum;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { s_hist[4 * tid + i] = run; run += v[i]; }
+  }
+  __syncthreads();
+  uint4 *out = reinterpret_cast<uint4 *>(a.tile_order);
+  for (int c = 0; c < chunks; ++c) {
+    if (chunks > 1) load(c);
+#pragma unroll
+    for (int j = 0; j < kOrdIpt; ++j) {
+      const int t = c * kOrdChunk + j * kOrdThreads + tid;
+      const bool valid = t < n;
+      const uint32_t bk = bucket(key[j]);
+      const unsigned long long peers = match_digit(bk, 8, __ballot(valid));
+      const uint32_t rank = (uint32_t)__popcll(peers & lt);
+      uint32_t base = 0;
+      if (valid && rank == 0) base = atomicAdd(&s_hist[bk], (uint32_t)__popcll(peers));
+      base = (uint32_t)__shfl((int)base, valid ? (int)__ffsll((long long)peers) - 1 : 0, kWave);
+      if (valid) out[base + rank] = make_uint4((uint32_t)t, rg[j].x, rg[j].y, 0u);
+    }
+  }
+  const int padded = (n + 7) & ~7;
+  for (int p = n + tid; p < padded; p += kOrdThreads) out[p] = make_uint4((uint32_t)n, 0u, 0u, 0u);
 }
 
 // ======================================================== blend bwd =======
@@ -1335,6 +1502,7 @@ __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
 
 template <bool kT16>
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
+  GS_WAVE_TIMER(1);
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
 #if GS_BWD_CHUNK_STAGE
@@ -1347,7 +1515,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
   const int ncell = cg.cells();
   int tile, quad;
-  cell_tile(blockIdx.x, ncell, tile, quad);
+  uint32_t start, lend;
+  cell_tile(blockIdx.x, ncell, a.tile_order, a.ranges, a.tiles_x * a.tiles_y, tile, quad, start, lend);
   if (tile >= a.tiles_x * a.tiles_y) return;
   const int lane = threadIdx.x;
   const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
@@ -1356,8 +1525,6 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
   const int W = a.cam.image_width, H = a.cam.image_height;
   const bool inside = cx0 + (lane & 7) < cg.L && cy0 + (lane >> 3) < cg.L && px < W && py < H;
-  const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]);
-  const uint32_t lend = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
   if (start >= lend) return;  // empty list: no gradient here (and no entry to read speculatively)
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   // The prologue's loads in two round trips, without branches (a load under
@@ -2608,6 +2775,24 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   return check_launch("gs_blend_forward");
 }
 
+size_t gs_tile_order_size(int32_t num_tiles) { return num_tiles > 0 ? 4u * (size_t)((num_tiles + 7) & ~7) : 0; }
+
+gs_status gs_tile_order(const gs_order_args *a, gs_stream_t stream) {
+  if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_tile_order");
+  if (a->num_tiles < 0 || (a->cell_work && (a->cells < 1 || a->cells > 1024)))
+    return fail(GS_ERR_INVALID_ARG, "%s: bad num_tiles / cells", "gs_tile_order");
+  if (a->num_tiles == 0) return GS_OK;
+  if (!a->tile_order || !a->ranges) return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_order");
+  hipStream_t s = (hipStream_t)stream;
+  if (!a->cell_work)
+    k_tile_order<0><<<1, kOrdThreads, 0, s>>>(*a);
+  else if (a->cells == 4)
+    k_tile_order<1><<<1, kOrdThreads, 0, s>>>(*a);
+  else
+    k_tile_order<2><<<1, kOrdThreads, 0, s>>>(*a);
+  return check_launch("gs_tile_order");
+}
+
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_backward");
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_blend_backward");
@@ -2692,5 +2877,18 @@ gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream) {
       c, make_int4(starts[0], starts[1], starts[2], starts[3]), make_int4(starts[4], starts[5], starts[6], starts[7]));
   return check_launch("gs_adam_step");
 }
+
+#ifdef GS_WAVE_TIMES
+// (variant builds only) which = 0: the last k_blend_fwd, 1: the last
+// k_blend_bwd; per workgroup (start, end, xcc << 32 | HW_ID), u64 each
+gs_status gs_debug_wave_times(int32_t which, void *host, size_t bytes) {
+  if (which < 0 || which > 1 || bytes > sizeof(g_wave_times[0]))
+    return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_debug_wave_times");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_times), bytes, (size_t)which * sizeof(g_wave_times[0]),
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(GS_ERR_LAUNCH, "%s: copy failed", "gs_debug_wave_times");
+  return GS_OK;
+}
+#endif
 
 }  // extern "C"

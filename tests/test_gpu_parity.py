@@ -2,7 +2,8 @@
 reference's golden vectors and the pinned CPU oracle.
 
 Tolerances are in tests/golden_io.py (1e-4 abs on image/alpha, gated depth,
-grads 2e-3 x max|ref| + 1e-5)."""
+grads 1e-4 x max|ref| + 1e-7 outside knife-edge-touched Gaussians)."""
+import ctypes as C
 import math
 
 import numpy as np
@@ -362,6 +363,53 @@ def test_deterministic(pkg, cuda):
         res.append((out["image"].clone(), m._xyz.grad.clone(), m._rotation.grad.clone()))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("tile", [16, 8])
+def test_tile_dispatch_order(pkg, cuda, monkeypatch, tile):
+    """gs_tile_order: a permutation of the tiles, heaviest key first (by its
+    256 buckets), padded to a multiple of 8 with num_tiles; and the blend
+    launches give bit-identical frames and gradients in any dispatch order
+    (none, forward only, backward only, both)."""
+    RZ, N = pkg.rasterizer, pkg._native
+    lib = N.load()
+    syn = pkg.synthetic
+    W, H = 328, 250  # partial edge tiles, tiles not a multiple of 8
+    sc = syn.make_scene(30000, W, H, seed=8, sigma_range=(0.002, 0.03))
+    res = []
+    for fwd, bwd in ((False, False), (True, False), (False, True), (True, True)):
+        monkeypatch.setattr(RZ, "_ORDER_FWD", fwd)
+        monkeypatch.setattr(RZ, "_ORDER_BWD", bwd)
+        m = syn.to_model(sc, pkg.GaussianModel, cuda)
+        out = pkg.GaussianRenderer(tile_size=tile).render(Cam(W, H, sc.fovx, sc.fovy), m,
+                                                          pkg.RenderSettings(H, W, torch.zeros(3)))
+        (out["image"].sum() + out["alpha"].sum()).backward()
+        res.append((out["image"].clone(), out["alpha"].clone(), m._xyz.grad.clone(), m._opacity.grad.clone(),
+                    m._scaling.grad.clone()))
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert torch.equal(a, b)
+    # the order itself, on a random ranges table and on random cell work
+    nt = 1021
+    g = torch.Generator().manual_seed(3)
+    lens = torch.randint(0, 5000, (nt,), generator=g, dtype=torch.int32)
+    lens[::7] = 0
+    starts = torch.cumsum(lens, 0, dtype=torch.int32) - lens
+    ranges = torch.stack([starts, starts + lens], 1).to(cuda)
+    work = torch.randint(0, 900, (nt, 4), generator=g, dtype=torch.int32)
+    rc = ranges.cpu().long()
+    for key, cw in ((lens.long(), None), (work.long().sum(1), work.to(cuda))):
+        out = torch.full((int(lib.gs_tile_order_size(nt)),), -1, dtype=torch.int32, device=cuda)
+        oa = N.GsOrderArgs(nt, 4, N.ptr(ranges), N.ptr(cw), N.ptr(out))
+        N.check(lib.gs_tile_order(C.byref(oa), None), "gs_tile_order")
+        e = out.cpu().long().view(-1, 4)
+        o = e[:, 0]
+        assert e.shape[0] == 1024 and bool((o[nt:] == nt).all())
+        assert sorted(o[:nt].tolist()) == list(range(nt))
+        assert torch.equal(e[:nt, 1:3], rc[o[:nt]]) and bool((e[:, 3] == 0).all())  # each tile's range
+        # keys descending up to the width of one of the 256 buckets
+        k = key[o[:nt]]
+        assert bool((k[:-1] + (int(key.max()) + 1) // 256 + 1 >= k[1:]).all())
 
 
 def test_emit_capacity_guess(pkg, cuda):
