@@ -1578,6 +1578,10 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   // PG = P + G0 carried as one running sum (a gradient factor, no decision)
   float PG = ((gR0 * bg0 + gR1 * bg1) + gR2 * bg2) + G0;
   float A = 0.f, T1 = 1.f;  // T1 = 1 - A, carried: the next entry's transmittance is this one's rcp argument
+  // running (A < 0.995 so far; lanes outside the image never run): replays
+  // the forward's per-lane termination, so an entry past the pixel's n_eval
+  // is never taken
+  bool run = inside;
   const uint32_t nwords = (wstop + 63u) >> 6;
   // liveness word wd of this quadrant, cut at wstop (bits past it were never written)
   auto live_word = [&](uint32_t wd) -> unsigned long long {
@@ -1744,7 +1748,6 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       const uint32_t bit = (uint32_t)__builtin_ctzll(m);
       m &= m - 1ull;
       cm |= 1ull << bit;
-      const uint32_t i = 64u * wd + bit;
       // two b128 broadcasts and a b64: (mx my q00 q11) (qo o r g) (b z);
       // pq = (q00, q11), po = (qo, opacity)
       const float4 r0v = reinterpret_cast<const float4 *>(cb + 48 * kk)[0];
@@ -1754,8 +1757,10 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       const float2 po = make_float2(r1v.x, r1v.y), prg = make_float2(r1v.z, r1v.w);
       const float dx = fx - pm.x, dy = fy - pm.y;
       const float sq = conic_s(dx, dy, pq.x, po.x, pq.y);
-      // the w < 1e-5 skip on s, as in the forward (NaN falls through)
-      const bool live = (i < neval) && !(sq > kSkipS);
+      // the w < 1e-5 skip on s, as in the forward (NaN falls through); `run`
+      // is the forward's "A < 0.995 before this entry", carried from the
+      // previous entry's own test -- the same decisions as i < n_eval
+      const bool live = run && !(sq > kSkipS);
       const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
       const bool simple = kAllSimple || ((simple_w >> bit) & 1ull);
       float dop, cw;
@@ -1774,7 +1779,9 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float inv = __builtin_amdgcn_rcpf(T1);  // v_rcp_f32 (1 ulp): a gradient factor, no decision
         const float d_live = __builtin_fmaf(inv, PG, X);
         // the terminating contributor has nothing behind it: (1-A_total)/T_{i+1} = 1
-        const float dal = trans * (A >= kAlphaStop ? X + gA : d_live);
+        const bool stop = !(A < kAlphaStop);
+        const float dal = trans * (stop ? X + gA : d_live);
+        run = run && !stop;
         dop = dal * wv;
         cw = c;
       } else {
@@ -1788,12 +1795,13 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
         const float c = trans * (live ? ai : 0.f);
         A = A + c;
         PG = __builtin_fmaf(c, X, PG);
-        const bool term = A >= kAlphaStop;
+        const bool term = !(A < kAlphaStop);
         T1 = 1.f - A;
         // both arms computed, then a select: no divergent branch per entry
         const float inv = __builtin_amdgcn_rcpf(T1);
         const float d_live = __builtin_fmaf(inv, PG, X);
         const float dal = trans * (term ? X + gA : d_live);
+        run = run && !term;
         // u = o*w >= 0, so "u in [0,1]" (the clamp passes the gradient) is ai == u;
         // e = exp(.) >= 0, so "e in [0,1]" is w == e (both false for NaN)
         const float g = (ai == u) ? dal * w : 0.f;
