@@ -245,6 +245,24 @@ def check(status: int, what: str):
         raise RuntimeError(f"{what} failed (gs_status={status}): {msg}")
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def stream_ptr(device=None) -> int:
+    """The current HIP stream of `device` (default: the current device), as
+    the integer handle the C ABI takes.  Through torch's raw-stream accessor:
+    torch.cuda.current_stream() builds a Stream object per call (~12 us of
+    host time on the box), and the render, the optimizer and every gradient
+    range's collective ask for the stream."""
+    if _RAW_STREAM is not None:
+        if device is None or getattr(device, "index", None) is None:
+            idx = torch.cuda.current_device()
+        else:
+            idx = device.index
+        return int(_RAW_STREAM(idx))
+    return torch.cuda.current_stream(device).cuda_stream
+
+
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 

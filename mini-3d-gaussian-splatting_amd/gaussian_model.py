@@ -226,7 +226,7 @@ class GaussianModel(nn.Module):
         a.adam_m_in = arrays([st.get("exp_avg") for st in states])
         a.adam_v_in = arrays([st.get("exp_avg_sq") for st in states])
         a.workspace, a.workspace_bytes, a.counters = N.ptr(ws), ws.numel(), N.ptr(counters)
-        stream = torch.cuda.current_stream().cuda_stream
+        stream = N.stream_ptr()
         N.check(lib.gs_densify_count(C.byref(a), stream), "gs_densify_count")
         kept, nsplit, ncl, n_out = (int(v) for v in counters.tolist())
         outs = [torch.empty((n_out,) + tuple(p.shape[1:]), dtype=p.dtype, device=dev) for p in params]

@@ -49,7 +49,7 @@ class _FusedPhotometric(torch.autograd.Function):
         maps = torch.empty((3, Cn, H, W), dtype=torch.float32, device=dev) if need_grad else None
         a = N.GsLossArgs(Cn, H, W, N.ptr(pred), N.ptr(target), float(lambda_dssim), int(window), _C1, _C2,
                          N.ptr(ws), ws.numel(), N.ptr(maps), N.ptr(out), None, None)
-        N.check(lib.gs_loss_forward(C.byref(a), torch.cuda.current_stream().cuda_stream), "gs_loss_forward")
+        N.check(lib.gs_loss_forward(C.byref(a), N.stream_ptr()), "gs_loss_forward")
         ctx.save_for_backward(pred, target, maps)
         ctx.lam, ctx.window = float(lambda_dssim), int(window)
         return out
@@ -65,7 +65,7 @@ class _FusedPhotometric(torch.autograd.Function):
         d_pred = torch.empty_like(pred)
         a = N.GsLossArgs(Cn, H, W, N.ptr(pred), N.ptr(target), ctx.lam, ctx.window, _C1, _C2,
                          None, 0, N.ptr(maps), None, N.ptr(g_total), N.ptr(d_pred))
-        N.check(lib.gs_loss_backward(C.byref(a), torch.cuda.current_stream().cuda_stream), "gs_loss_backward")
+        N.check(lib.gs_loss_backward(C.byref(a), N.stream_ptr()), "gs_loss_backward")
         return d_pred, None, None, None, None
 
 

@@ -62,7 +62,7 @@ class FusedAdam(torch.optim.Optimizer):
         """One gs_adam_step per (betas, eps) batch of <= 8 tensors, over rows
         [lo, hi) of each (dim 0; all rows when lo is None)."""
         lib = N.load()
-        stream = torch.cuda.current_stream().cuda_stream
+        stream = N.stream_ptr()
         for (b1, b2, eps), ds in batches.items():
             for i in range(0, len(ds), N.GS_ADAM_MAX_TENSORS):
                 chunk = ds[i:i + N.GS_ADAM_MAX_TENSORS]

@@ -120,7 +120,7 @@ def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return N.stream_ptr()
 
 
 class StageTimer:

@@ -28,6 +28,8 @@ from typing import List, Sequence, Tuple
 
 import torch
 
+from . import _native
+
 NCCL_FLOAT32 = 7
 NCCL_SUM, NCCL_AVG = 0, 4
 HIP_EVENT_DISABLE_TIMING = 0x2
@@ -122,7 +124,7 @@ class RcclComm:
         queued so far on the current stream, on the collective stream."""
         rccl, hip = self._rccl, self._hip
         ready, done = self._events(k)
-        comp = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        comp = C.c_void_p(_native.stream_ptr(self.device))
         coll = C.c_void_p(self._stream.cuda_stream)
         _check_hip(hip.hipEventRecord(ready, comp), "hipEventRecord")
         _check_hip(hip.hipStreamWaitEvent(coll, ready, 0), "hipStreamWaitEvent")
@@ -142,7 +144,7 @@ class RcclComm:
 
     def wait(self, k: int) -> None:
         """The current stream waits for range k's collective (host does not block)."""
-        comp = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        comp = C.c_void_p(_native.stream_ptr(self.device))
         _check_hip(self._hip.hipStreamWaitEvent(comp, self._done[k], 0), "hipStreamWaitEvent")
 
     def close(self) -> None:
