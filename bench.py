@@ -68,8 +68,8 @@ def parse():
     ap.add_argument("--spinup-steps", type=int, default=50,
                     help="untimed steps before the --warmup steps, for the GPU clock ramp")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="oracle threads (capped by the CPUs this process may run on); the box's share is 16")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="an extra oracle thread count for the CPU sweep (16..256 and the CPU limit always run)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI) for the driver; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--force-dist", action="store_true",
@@ -320,7 +320,10 @@ def main():
             nsteps = a.spinup_steps + a.warmup + a.steps + a.diag_steps
             line["allreduce"] = {"ranges_per_step": reducer.overlap_chunks(), "pipelined_adam": opt is not None,
                                  "host_us_per_step": {k: round(1e6 * v / nsteps, 1) for k, v in reducer.host_s.items()},
-                                 "avg": reducer._avg}
+                                 "avg": reducer._avg, "native": reducer.native_status["native"],
+                                 "rccl_nranks": reducer.native_status["rccl_nranks"],
+                                 "self_check_err": reducer.native_status["self_check_err"],
+                                 "fallback_reason": reducer.native_status["fallback_reason"]}
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
@@ -375,30 +378,83 @@ def pmc_traffic(stage):
     return int(2 * fetch + write), info
 
 
+def cpu_limit():
+    """The CPUs this process may use: sched_getaffinity, and the cgroup v2
+    quota (cpu.max "quota period"; "max" = none) of its own cgroup.  Returns
+    (usable CPUs, info dict)."""
+    avail = len(os.sched_getaffinity(0))
+    info = {"nproc": os.cpu_count(), "sched_getaffinity": avail, "cgroup_cpu_max": None,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    limit = avail
+    try:
+        v2, v1 = "/", "/"
+        for ln in open("/proc/self/cgroup"):
+            parts = ln.strip().split(":", 2)
+            if len(parts) == 3 and parts[0] == "0":  # the v2 unified hierarchy
+                v2 = parts[2]
+            elif len(parts) == 3 and "cpu" in parts[1].split(","):  # v1 cpu controller
+                v1 = parts[2]
+        quota = None
+        for d in (os.path.join("/sys/fs/cgroup", v2.lstrip("/")), "/sys/fs/cgroup"):
+            p = os.path.join(d, "cpu.max")
+            if os.path.exists(p):
+                raw = open(p).read().strip()
+                info["cgroup_cpu_max"] = raw
+                q, per = raw.split()[:2]
+                quota = None if q == "max" else (int(q), int(per))
+                break
+        else:
+            for d in (os.path.join("/sys/fs/cgroup/cpu", v1.lstrip("/")), "/sys/fs/cgroup/cpu"):
+                p = os.path.join(d, "cpu.cfs_quota_us")
+                if os.path.exists(p):
+                    q, per = int(open(p).read()), int(open(os.path.join(d, "cpu.cfs_period_us")).read())
+                    info["cgroup_cpu_max"] = f"v1 cfs_quota_us={q} cfs_period_us={per}"
+                    quota = (q, per) if q > 0 else None
+                    break
+        if quota:
+            limit = min(limit, max(1, int(math.ceil(quota[0] / quota[1]))))
+    except (OSError, ValueError):
+        pass
+    info["limit"] = limit
+    return limit, info
+
+
 def cpu_baseline(scene, W, H, cot, threads):
     """Oracle (C restatement of the reference render path) fwd+bwd on the
-    host cores for the same C3 frame, then on one core; bounded: one frame
-    each (~1 s and ~15 s)."""
+    host cores for the same C3 frame: one frame per thread count of a sweep
+    (16, 32, 64, 128, 256, capped by the CPUs this process may use, cgroup
+    quota included; `threads` > 0 adds that count), the fastest reported, then
+    one frame on one core.  Bounded: ~1 s per multi-thread frame, ~10 s on one
+    core."""
     import numpy as np
     from oracle import oracle as orc  # CPU baseline leg: test infrastructure only
-    avail = len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, avail))
+    limit, info = cpu_limit()
+    counts = sorted({c for c in (16, 32, 64, 128, 256, threads) if 0 < c <= limit} | {limit})
     cov = orc.covariance(scene.scaling.numpy(), scene.rotation.numpy())
     s = orc.Scene(xyz=scene.xyz.numpy(), cov3d=cov, color_logits=scene.features_dc[:, 0].numpy(),
                   opacity=torch.sigmoid(scene.opacity[:, 0]).numpy(), wv=np.eye(4), width=W, height=H,
                   fovx=scene.fovx, fovy=scene.fovy, bg=np.zeros(3, np.float32))
     gi, ga, gd = (c.cpu().numpy() for c in cot)
-    t0 = time.perf_counter()
-    ref = orc.render_backward(s, gi, ga, gd, nthreads=threads)
-    dt = time.perf_counter() - t0
+    sweep, ref, best = {}, None, None
+    for c in counts:
+        t0 = time.perf_counter()
+        r = orc.render_backward(s, gi, ga, gd, nthreads=c)
+        dt = time.perf_counter() - t0
+        sweep[str(c)] = round(H * W / dt / 1e6, 4)
+        if ref is None:
+            ref = r
+        if best is None or dt < best[1]:
+            best = (c, dt)
     t0 = time.perf_counter()
     orc.render_backward(s, gi, ga, gd, nthreads=1)
     dt1 = time.perf_counter() - t0
+    threads, dt = best
     return {"value": round(H * W / dt / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"one full C3 frame ({W}x{H}, {scene.xyz.shape[0]} Gaussians) fwd+bwd, "
-                      f"oracle/gs_oracle.c with OpenMP x{threads} ({dt:.2f} s) and on 1 core ({dt1:.2f} s)",
+            "sample": f"one full C3 frame ({W}x{H}, {scene.xyz.shape[0]} Gaussians) fwd+bwd per thread count, "
+                      f"oracle/gs_oracle.c with OpenMP; fastest x{threads} ({dt:.2f} s), 1 core ({dt1:.2f} s)",
+            "thread_sweep_mpix_s": sweep, "cpu_limit": info,
             "one_core": {"value": round(H * W / dt1 / 1e6, 4), "unit": "Mpix/s", "cores": 1},
-            "host_cpus_schedulable": avail}, ref["image"]
+            "host_cpus_schedulable": info["sched_getaffinity"]}, ref["image"]
 
 
 def reference_cost_model(H, W, M, E, C):

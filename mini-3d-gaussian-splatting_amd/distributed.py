@@ -37,22 +37,70 @@ import torch
 
 
 _NATIVE_COMMS: dict = {}
+NATIVE_STATUS: dict = {}  # key -> {"native", "rccl_nranks", "self_check_err", "fallback_reason"}
+_ATEXIT = False
 
 
-def _native_comm(dist, group):
-    """The process group's RcclComm on the current device (created once, on
-    every rank together: the first GradAllReduce is built at the same
-    iteration everywhere), or None if RCCL cannot be driven directly."""
-    key = (id(group if group is not None else dist.group.WORLD), torch.cuda.current_device())
+def _agreement(dist, group, device):
+    """agree(ok) -> the logical AND of `ok` over the group's ranks (one int32
+    MIN all-reduce through torch.distributed on `device`)."""
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        return bool(int(t.item()))
+    return agree
+
+
+def _native_comm(dist, group, factory=None, device=None):
+    """The process group's RcclComm on the current device, or None -- decided
+    by all ranks together (rccl.RcclComm: every construction step that can
+    fail on some ranks only is followed by an all-ranks agreement, so either
+    every rank drives RCCL natively or every rank falls back to
+    torch.distributed; never a mix, whose collectives would not match).
+    Created once per (group, device), on every rank at the same point (the
+    first GradAllReduce is built at the same iteration everywhere).  The
+    outcome is kept in NATIVE_STATUS for the bench line.  `factory` and
+    `device` are for tests (a fake communicator over gloo on the CPU)."""
+    global _ATEXIT
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    key = (id(group if group is not None else dist.group.WORLD), str(device))
     if key not in _NATIVE_COMMS:
-        try:
-            from .rccl import RcclComm
-            _NATIVE_COMMS[key] = RcclComm(dist, group)
-        except Exception as e:  # e.g. no librccl beside torch: the torch.distributed path
+        coll_dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        agree = _agreement(dist, group, coll_dev)
+        comm, reason = None, None
+        if factory is None:
+            try:
+                from .rccl import RcclComm as factory
+            except Exception as e:  # noqa: BLE001 -- this rank cannot; tell the others at step 1
+                reason = f"import rccl: {e}"
+                agree(False)
+        if factory is not None:
+            try:
+                comm = factory(dist, group, device=device, agree=agree, coll_device=coll_dev)
+            except Exception as e:  # noqa: BLE001 -- raised on every rank at the same step
+                reason = str(e)
+        if comm is None:
             import warnings
-            warnings.warn(f"native RCCL unavailable ({e}); gradient all-reduce through torch.distributed")
-            _NATIVE_COMMS[key] = None
+            warnings.warn(f"native RCCL not used ({reason}); gradient all-reduce through torch.distributed "
+                          "on every rank")
+        NATIVE_STATUS[key] = {"native": comm is not None,
+                              "rccl_nranks": getattr(comm, "nranks", None),
+                              "self_check_err": getattr(comm, "self_check", None),
+                              "fallback_reason": reason}
+        _NATIVE_COMMS[key] = comm
+        if comm is not None and not _ATEXIT:
+            # left to process-exit teardown, the communicators would go after
+            # the HIP runtime; callers that tear down earlier call it themselves
+            import atexit
+            atexit.register(close_native_comms)
+            _ATEXIT = True
     return _NATIVE_COMMS[key]
+
+
+def native_status() -> Optional[dict]:
+    """The last native-communicator decision (None before any)."""
+    return next(reversed(NATIVE_STATUS.values())) if NATIVE_STATUS else None
 
 
 def close_native_comms() -> None:
@@ -105,14 +153,21 @@ class GradAllReduce:
         self.ranges_reduced = 0  # rows_ready calls so far (diagnostic)
         self.host_s = {"rows_ready": 0.0, "reduce_and_step": 0.0}  # host seconds spent issuing (diagnostic)
         # RCCL (backend "nccl") forms the mean inside the reduction (ReduceOp.AVG,
-        # NCCL >= 2.10); gloo has no AVG: SUM, then one division.  Decided once.
+        # NCCL >= 2.10; this image's RCCL is 2.27); gloo has no AVG: SUM, then one
+        # division.  Decided once, here, from the backend: a collective that
+        # fails later is an error, never retried with another op (a retry on
+        # one rank would issue a collective the others never do).
         self._avg: bool = (dist.is_initialized() and dist.get_backend(group) == "nccl"
                            and hasattr(dist.ReduceOp, "AVG")) if hasattr(dist, "is_initialized") else False
         # backend "nccl": the collectives go to RCCL directly (rccl.RcclComm, one
-        # communicator per process group and device, ncclAvg), unless GS_DP_NATIVE=0
+        # communicator per process group and device, ncclAvg, established and
+        # self-checked by all ranks together), unless GS_DP_NATIVE=0
         self._native = None
+        self.native_status = {"native": False, "rccl_nranks": None, "self_check_err": None,
+                              "fallback_reason": "GS_DP_NATIVE=0" if self._avg else "backend is not nccl"}
         if self._avg and os.environ.get("GS_DP_NATIVE", "1") != "0":
             self._native = _native_comm(dist, group)
+            self.native_status = dict(native_status())
 
     def _bucket(self) -> torch.Tensor:
         sizes = [p.numel() for p in self.params]
@@ -232,13 +287,8 @@ class GradAllReduce:
             return self._copy_out(views, in_place)
         if self._avg:
             # RCCL divides inside the reduction: no extra pass over the bucket
-            try:
-                self.dist.all_reduce(flat, op=self.dist.ReduceOp.AVG, group=self.group)
-            except RuntimeError:
-                # a backend that has the enum but rejects AVG at run time: SUM and
-                # one division from now on (the failed call reduced nothing)
-                self._avg = False
-        if not self._avg:
+            self.dist.all_reduce(flat, op=self.dist.ReduceOp.AVG, group=self.group)
+        else:
             self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
             flat.div_(world)
         self._copy_out(views, in_place)

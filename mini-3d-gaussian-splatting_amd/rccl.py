@@ -19,6 +19,19 @@ its own over the process group's ranks:
 The unique id travels through the torch process group once (a 128-byte
 broadcast).  Every rank issues the same ranges in the same order, as
 collectives must match.
+
+Establishing the communicator is a collective decision (every rank takes the
+native path, or none does): construction runs four steps -- load the
+libraries, make the unique id (rank 0; its status rides on the id's
+broadcast), ncclCommInitRank, a self-check collective -- and after each step
+that can fail on some ranks only, the ranks all-reduce an "ok" flag over the
+torch process group (`agree`).  A step that failed anywhere raises RcclError on
+every rank at the same point, so the caller (distributed._native_comm) falls
+back to torch.distributed on all ranks together.  The self-check runs the
+production call shape -- a grouped ncclAllReduce of two slices at non-zero
+offsets with ncclAvg on the collective stream behind an event -- on
+rank-dependent integer-valued data, checks the mean on every rank, and checks
+ncclCommCount / ncclCommUserRank against the process group.
 """
 from __future__ import annotations
 
@@ -58,10 +71,13 @@ def _libs():
         rccl.ncclGroupStart.argtypes = []
         rccl.ncclGroupEnd.argtypes = []
         rccl.ncclCommDestroy.argtypes = [vp]
+        rccl.ncclCommAbort.argtypes = [vp]
+        rccl.ncclCommCount.argtypes = [vp, C.POINTER(C.c_int)]
+        rccl.ncclCommUserRank.argtypes = [vp, C.POINTER(C.c_int)]
         rccl.ncclGetErrorString.argtypes = [C.c_int]
         rccl.ncclGetErrorString.restype = C.c_char_p
         for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclGroupStart", "ncclGroupEnd",
-                  "ncclCommDestroy"):
+                  "ncclCommDestroy", "ncclCommAbort", "ncclCommCount", "ncclCommUserRank"):
             getattr(rccl, f).restype = C.c_int
         hip.hipEventCreateWithFlags.argtypes = [C.POINTER(vp), C.c_uint]
         hip.hipEventRecord.argtypes = [vp, vp]
@@ -87,28 +103,115 @@ def _check_hip(r: int, what: str):
         raise RcclError(f"{what}: hipError {r}")
 
 
+SELF_CHECK_COUNT = 1027  # elements of the self-check buffer (two slices: 600 + 427)
+
+
 class RcclComm:
     """An RCCL communicator over the ranks of `group` (torch process group of
-    backend "nccl"), with its own collective stream and per-range events."""
+    backend "nccl"), with its own collective stream and per-range events.
 
-    def __init__(self, dist, group=None, device=None):
-        rccl, hip = _libs()
-        self._rccl, self._hip = rccl, hip
+    `agree(ok) -> bool` is the ranks' logical AND of `ok` (an all-reduce over
+    the process group, distributed._agreement); without it each rank decides
+    alone (world size 1, or tests).  `coll_device` is where the process
+    group's collectives take their tensors (cuda for nccl, cpu for gloo).
+    Attributes after construction: nranks (ncclCommCount), self_check (the
+    largest relative error of the check's mean)."""
+
+    def __init__(self, dist, group=None, device=None, agree=None, coll_device=None):
+        agree = agree if agree is not None else (lambda ok: ok)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._coll_device = coll_device if coll_device is not None else self.device
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        uid = _UniqueId()
-        if self.rank == 0:
-            _check_nccl(rccl, rccl.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
-        buf = torch.frombuffer(bytearray(C.string_at(C.addressof(uid), 128)), dtype=torch.uint8).to(self.device)
-        src = dist.get_global_rank(group, 0) if group is not None else 0
-        dist.broadcast(buf, src=src, group=group)
-        C.memmove(C.addressof(uid), bytes(buf.cpu().numpy().tobytes()), 128)
         self._comm = C.c_void_p()
-        _check_nccl(rccl, rccl.ncclCommInitRank(C.byref(self._comm), self.world, uid, self.rank), "ncclCommInitRank")
-        self._stream = torch.cuda.Stream(device=self.device)
         self._ready: List[C.c_void_p] = []
         self._done: List[C.c_void_p] = []
+        self._stream = None
+        self.nranks = None
+        self.self_check = None
+
+        def step(what, fn):
+            err = None
+            try:
+                fn()
+            except Exception as e:  # noqa: BLE001 -- every failure is decided collectively below
+                err = f"{what}: {e}"
+            if not agree(err is None):
+                self._abort()
+                raise RcclError(err or f"{what} failed on another rank")
+
+        # 1. the libraries (and a stream of our own)
+        step("load", self._load)
+        # 2. the unique id: rank 0 makes it; its status rides on the broadcast
+        uid = _UniqueId()
+        ok, err0 = 1, None
+        if self.rank == 0:
+            try:
+                self._get_unique_id(uid)
+            except Exception as e:  # noqa: BLE001
+                ok, err0 = 0, f"ncclGetUniqueId: {e}"
+        raw = bytearray(C.string_at(C.addressof(uid), 128)) + bytearray([ok])
+        buf = torch.frombuffer(raw, dtype=torch.uint8).to(self._coll_device)
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(buf, src=src, group=group)
+        got = bytes(buf.cpu().numpy().tobytes())
+        if got[128] != 1:
+            self._abort()
+            raise RcclError(err0 or "ncclGetUniqueId failed on rank 0")
+        C.memmove(C.addressof(uid), got[:128], 128)
+        # 3. the communicator; 4. the self-check collective
+        step("ncclCommInitRank", lambda: self._init_comm(uid))
+        step("self-check", self._self_check)
+
+    # -- construction steps (overridable: tests drive the protocol with fakes) --
+    def _load(self) -> None:
+        self._rccl, self._hip = _libs()
+        self._stream = torch.cuda.Stream(device=self.device)
+
+    def _get_unique_id(self, uid: "_UniqueId") -> None:
+        _check_nccl(self._rccl, self._rccl.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
+
+    def _init_comm(self, uid: "_UniqueId") -> None:
+        rccl = self._rccl
+        _check_nccl(rccl, rccl.ncclCommInitRank(C.byref(self._comm), self.world, uid, self.rank), "ncclCommInitRank")
+        cnt, me = C.c_int(-1), C.c_int(-1)
+        _check_nccl(rccl, rccl.ncclCommCount(self._comm, C.byref(cnt)), "ncclCommCount")
+        _check_nccl(rccl, rccl.ncclCommUserRank(self._comm, C.byref(me)), "ncclCommUserRank")
+        if cnt.value != self.world or me.value != self.rank:
+            raise RcclError(f"communicator has {cnt.value} ranks (this one {me.value}); "
+                            f"the process group {self.world} (this one {self.rank})")
+        self.nranks = cnt.value
+
+    def _self_check(self) -> None:
+        """The production call shape on known values: x_i = (rank + 1)(i mod 97
+        + 1) in two slices, mean-reduced as range 0 behind an event; the mean
+        is (world + 1) / 2 (i mod 97 + 1) on every rank (integer sums: exact in
+        any order; ncclAvg's scaling by 1 / world rounds once)."""
+        n, cut = SELF_CHECK_COUNT, 600
+        base = (torch.arange(n, dtype=torch.float32, device=self.device) % 97) + 1
+        x = base * float(self.rank + 1)
+        ptr = x.data_ptr()
+        self.all_reduce(0, [(ptr, cut), (ptr + 4 * cut, n - cut)], avg=True)
+        self.wait(0)
+        torch.cuda.synchronize(self.device)
+        want = base * (self.world + 1) / 2.0
+        err = float(((x - want).abs() / want).max())
+        self.self_check = err
+        if not err <= 1e-6:
+            raise RcclError(f"self-check mean off by {err:.3g} (relative)")
+
+    def _abort(self) -> None:
+        """Drop a half-built communicator without waiting for other ranks."""
+        rccl, hip = getattr(self, "_rccl", None), getattr(self, "_hip", None)
+        if self._comm and rccl is not None:
+            try:
+                rccl.ncclCommAbort(self._comm)
+            finally:
+                self._comm = C.c_void_p()
+        if hip is not None:
+            for ev in self._ready + self._done:
+                hip.hipEventDestroy(ev)
+        self._ready, self._done = [], []
 
     def _events(self, k: int):
         while len(self._ready) <= k:

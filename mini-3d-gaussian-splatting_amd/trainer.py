@@ -128,6 +128,16 @@ class GaussianTrainer:
             self._reducer = None
         return {"loss": total.detach(), "l1": l1, "dssim": dssim}
 
+    def close(self) -> None:
+        """Tear down the data-parallel transport: the native RCCL communicators
+        go before the caller destroys the process group (every rank calls this
+        at the same point, after its last step).  Also registered at exit by
+        distributed._native_comm."""
+        if self._dist is not None:
+            from .distributed import close_native_comms
+            close_native_comms()
+        self._reducer = None
+
     # -- loop (trainer.py:46-63) -------------------------------------------
     def train(self, iterations: Optional[int] = None) -> None:
         if self.gaussians is None:

@@ -243,3 +243,110 @@ def test_covers_needs_every_bucket_parameter():
     assert red.covers(list(params))
     assert not red.covers(list(params)[:-1])
     assert not red.covers(list(params) + [m._features_rest])
+
+
+def _worker_native_decision(rank, world, port, q, fail):
+    """Drive distributed._native_comm over gloo with a fake communicator
+    (rccl.RcclComm's construction steps overridden) that fails step `fail`
+    (load / uid / init / check / import) on rank 1 only, or never."""
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import importlib
+        rccl = importlib.import_module(pkg.__name__ + ".rccl")
+        RcclComm, RcclError = rccl.RcclComm, rccl.RcclError
+        calls = []
+
+        class Fake(RcclComm):
+            def _load(self):
+                calls.append("load")
+                if fail == "load" and self.rank == 1:
+                    raise OSError("librccl.so: cannot open shared object file")
+
+            def _get_unique_id(self, uid):
+                calls.append("uid")
+                if fail == "uid":
+                    raise RcclError("ncclGetUniqueId: unhandled system error (2)")
+                uid.internal = b"fake-id"
+
+            def _init_comm(self, uid):
+                calls.append("init")
+                assert uid.internal.startswith(b"fake-id")  # rank 0's id reached every rank
+                if fail == "init" and self.rank == 1:
+                    raise RcclError("ncclCommInitRank: invalid usage (5)")
+                self.nranks = self.world
+
+            def _self_check(self):
+                calls.append("check")
+                if fail == "check" and self.rank == 1:
+                    raise RcclError("self-check mean off by 0.5 (relative)")
+                self.self_check = 0.0
+
+        factory = Fake
+        if fail == "import" and rank == 1:
+            # this rank cannot import the native module: the real _native_comm path
+            sys.modules[pkg.__name__ + ".rccl"] = None
+            factory = None
+        comm = pkg.distributed._native_comm(dist, None, factory=factory, device=torch.device("cpu"))
+        st = dict(pkg.distributed.native_status())
+        # the process group still works and every rank issues the same collectives
+        t = torch.tensor([float(rank + 1)])
+        dist.all_reduce(t)
+        pkg.distributed.close_native_comms()
+        q.put((rank, comm is not None, st, calls, float(t)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", [None, "load", "uid", "init", "check", "import"])
+def test_native_comm_decided_by_all_ranks_gloo(fail):
+    """Round-3 review item 3 / advisor: the native-RCCL choice is collective.
+    Whichever construction step fails on one rank (library load, rank 0's
+    unique id, communicator init, the self-check collective, the module
+    import), both ranks fall back to torch.distributed together, at the same
+    step, with the reason recorded -- no rank hangs in a broadcast and no mix
+    of transports; with no failure both take the native path and record the
+    communicator's rank count."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_native_decision, args=(r, 2, port, q, fail)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, native, st, calls, tsum = q.get(timeout=120)
+        res[r] = (native, st, calls, tsum)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0] == (fail is None)
+    for r in (0, 1):
+        native, st, calls, tsum = res[r]
+        assert tsum == 3.0
+        assert st["native"] == (fail is None)
+        if fail is None:
+            assert st["rccl_nranks"] == 2 and st["fallback_reason"] is None
+        else:
+            assert st["rccl_nranks"] is None and st["fallback_reason"]
+    # both ranks stop after the same step (rank 0 alone makes the unique id)
+    done = {None: ["load", "init", "check"], "load": ["load"], "uid": ["load"], "init": ["load", "init"],
+            "check": ["load", "init", "check"]}
+    if fail in done:
+        for r in (0, 1):
+            assert [c for c in res[r][2] if c != "uid"] == done[fail]
+        assert res[0][2].count("uid") == (0 if fail == "load" else 1) and "uid" not in res[1][2]
+    if fail == "load":
+        assert "another rank" in res[0][1]["fallback_reason"] and "librccl" in res[1][1]["fallback_reason"]
+    if fail == "check":
+        assert "another rank" in res[0][1]["fallback_reason"] and "self-check" in res[1][1]["fallback_reason"]
+    if fail == "uid":
+        assert "ncclGetUniqueId" in res[0][1]["fallback_reason"] and "rank 0" in res[1][1]["fallback_reason"]
+    if fail == "import":
+        assert "import rccl" in res[1][1]["fallback_reason"] and "another rank" in res[0][1]["fallback_reason"]
