@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 14
+#define GS_ABI_VERSION 15
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
@@ -249,11 +249,7 @@ typedef struct gs_blend_fwd_args {
   int64_t live_words;
   uint32_t *pair_counts;        /* [H*W] or NULL: each pixel's contributing pairs (c > 0), the
                                    work counter C of SURVEY 8(d); measurement only */
-  const uint32_t *tile_order;   /* [gs_tile_order_size] dispatch order (gs_tile_order), or NULL:
-                                   tiles in index order.  Outputs do not depend on it */
-  uint32_t *cell_work;          /* [num_tiles, gs_tile_quads] or NULL: per (tile, cell) the list
-                                   entries the backward will replay there (gs_tile_order's key
-                                   for the backward) */
+  int32_t num_pairs;            /* T, the entries of sorted_gauss: tile ranges are clamped to it */
 } gs_blend_fwd_args;
 gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
 
@@ -268,10 +264,8 @@ size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles);
 /* Cells per tile: ceil(tile_size / 8)^2 (4 for the default 16); 0 if out of range. */
 int32_t gs_tile_quads(int32_t tile_size);
 /* Gradient partials gs_blend_backward writes per list entry (G below): one
- * per 8x8 cell, gs_tile_quads(tile_size) (4 for the default 16x16 tile).  A
- * library built with -DGS_BWD_CPW=2 or 4 (measured slower)
- * adds 2 or 4 cells' sums of an entry on chip at the default tile and returns
- * 4 / GS_BWD_CPW there.  0 if out of range. */
+ * per 8x8 cell, gs_tile_quads(tile_size) (4 for the default 16x16 tile).
+ * 0 if out of range. */
 int32_t gs_partial_groups(int32_t tile_size);
 
 /* ---- Backward of the blend -------------------------------------------
@@ -282,10 +276,8 @@ int32_t gs_partial_groups(int32_t tile_size);
  * d_opacity, d_r, d_g, d_b, d_z} summed over group q's pixels, and sets
  * slot_live[G e + q] = 1; G = gs_partial_groups(tile_size), e = the entry's
  * gradient slot (pair_offset[g] + its tile's index in g's rectangle).  One
- * 64-lane workgroup per (tile, cell), and the group is the cell (the
- * GS_BWD_CPW variant builds replay 2 or 4 cells of a default tile per
- * workgroup, word by word).  Groups that did not replay the entry write
- * nothing.  No atomics: deterministic. */
+ * 64-lane workgroup per (tile, cell), and the group is the cell.  Groups
+ * that did not replay the entry write nothing.  No atomics: deterministic. */
 typedef struct gs_blend_bwd_args {
   gs_camera cam;
   int32_t tiles_x, tiles_y;
@@ -301,31 +293,9 @@ typedef struct gs_blend_bwd_args {
   int64_t live_words;
   float *pair_grads;            /* [T, G, GS_PARTIAL_STRIDE], G = gs_partial_groups(cam.tile_size) */
   uint8_t *slot_live;           /* [T, G], zeroed by the caller (or gs_tile_ranges) */
-  const uint32_t *tile_order;   /* dispatch order (gs_tile_order over the forward's cell_work), or
-                                   NULL.  Outputs do not depend on it */
+  int32_t num_pairs;            /* T, the entries of sorted_gauss: tile ranges are clamped to it */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
-
-/* ---- Dispatch order of the blend launches ------------------------------
- * No reference counterpart (scheduling only).  Lists the tiles by expected
- * work, largest first, so that the blend launches end on short workgroups
- * (their last round of workgroups otherwise leaves slots idle behind a few
- * long ones).  Key: the tile's list length (ranges), or, when cell_work is
- * given, the sum of its cells' replay counts from the forward.  Position p
- * holds 4 u32 (tile, start, end, 0), the tile and its list range, so a blend
- * workgroup reads both in one load.  Buckets of equal key in any order;
- * positions num_tiles .. ceil(num_tiles / 8) * 8 - 1 get tile = num_tiles
- * (skipped by the blend kernels).  One workgroup. */
-typedef struct gs_order_args {
-  int32_t num_tiles;
-  int32_t cells;               /* gs_tile_quads(tile_size), with cell_work */
-  const uint32_t *ranges;      /* [num_tiles, 2] (and the key when cell_work is NULL) */
-  const uint32_t *cell_work;   /* [num_tiles, cells] or NULL; 16-B aligned */
-  uint32_t *tile_order;        /* [gs_tile_order_size(num_tiles)] out, 16-B aligned */
-} gs_order_args;
-/* u32 words of tile_order: 4 x ceil(num_tiles / 8) * 8 */
-size_t gs_tile_order_size(int32_t num_tiles);
-gs_status gs_tile_order(const gs_order_args *a, gs_stream_t stream);
 
 /* ---- Backward of the projection ----------------------------------------
  * Sums each Gaussian's slot partials (slots [pair_offset[g], pair_offset[g]

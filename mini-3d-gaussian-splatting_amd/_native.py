@@ -27,7 +27,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 14
+GS_ABI_VERSION = 15
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -81,7 +81,7 @@ class GsBlendFwdArgs(C.Structure):
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
         ("sorted_gauss", _vp), ("records", _vp), ("image", _vp), ("alpha", _vp), ("depth", _vp),
         ("pix_acc", _vp), ("pix_state", _vp), ("live_bits", _vp), ("live_words", C.c_int64),
-        ("pair_counts", _vp), ("tile_order", _vp), ("cell_work", _vp),
+        ("pair_counts", _vp), ("num_pairs", C.c_int32),
     ]
 
 
@@ -91,14 +91,7 @@ class GsBlendBwdArgs(C.Structure):
         ("sorted_gauss", _vp), ("records", _vp), ("pix_acc", _vp),
         ("pix_state", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp),
         ("live_bits", _vp), ("live_words", C.c_int64), ("pair_grads", _vp), ("slot_live", _vp),
-        ("tile_order", _vp),
-    ]
-
-
-class GsOrderArgs(C.Structure):
-    _fields_ = [
-        ("num_tiles", C.c_int32), ("cells", C.c_int32), ("ranges", _vp), ("cell_work", _vp),
-        ("tile_order", _vp),
+        ("num_pairs", C.c_int32),
     ]
 
 
@@ -165,7 +158,7 @@ class GsDensifyArgs(C.Structure):
 EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
-    "gs_tile_ranges", "gs_tile_order_size", "gs_tile_order", "gs_blend_live_words", "gs_tile_quads", "gs_partial_groups", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
+    "gs_tile_ranges", "gs_blend_live_words", "gs_tile_quads", "gs_partial_groups", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
     "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
     "gs_densify_workspace_bytes", "gs_densify_count", "gs_densify_emit",
 )
@@ -194,9 +187,6 @@ def _declare(lib):
     lib.gs_bin_count.argtypes = [P(GsBinArgs), _vp]
     lib.gs_bin_emit.argtypes = [P(GsBinArgs), _vp]
     lib.gs_tile_ranges.argtypes = [P(GsRangeArgs), _vp]
-    lib.gs_tile_order_size.argtypes = [C.c_int32]
-    lib.gs_tile_order_size.restype = C.c_size_t
-    lib.gs_tile_order.argtypes = [P(GsOrderArgs), _vp]
     lib.gs_blend_live_words.argtypes = [C.c_int32, C.c_int32]
     lib.gs_blend_live_words.restype = C.c_size_t
     lib.gs_tile_quads.argtypes = [C.c_int32]

@@ -28,15 +28,12 @@ constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
-#ifndef GS_HIST_DIRECT_ATOMICS  // radix histogram: 1 = one LDS atomic per key, 0 = ballot-matched digits
-#define GS_HIST_DIRECT_ATOMICS 1
-#endif
-#ifndef GS_SORT_IPT
-#define GS_SORT_IPT 8
-#endif
-constexpr int kSortIpt = GS_SORT_IPT;            // items per thread per sort block
+constexpr int kSortIpt = 8;                      // items per thread per sort block (4, 16: slower)
 constexpr int kSortChunk = kBlock * kSortIpt;    // 2048 items per block
 constexpr int kBinChunk = kBlock * 4;            // 1024 Gaussians per binning block (2 and 1 rounds: slower)
+#ifndef GS_DEBUG  // 1: report (printf) blend list ranges clamped to the T entries
+#define GS_DEBUG 0
+#endif
 constexpr float kAlphaStop = 0.995f;             // renderer.py:352
 // renderer.py:336 skips a pair when w = exp(-s/2) < 1e-5; decided here on
 // s: s > 2 ln(1e5).  The same decision except where exp's rounding
@@ -62,33 +59,6 @@ gs_status check_launch(const char *what) {
 }
 
 inline unsigned div_up(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
-
-// Measurement-only (a variant build with -DGS_WAVE_TIMES, tools/wave_times.py):
-// each blend workgroup records its start and end on the 100 MHz real-time
-// clock and the XCD / CU it ran on, so the launch's occupancy over time and
-// its tail can be read back.  Not in the product build.
-#ifdef GS_WAVE_TIMES
-constexpr uint32_t kWtMax = 1u << 17;
-__device__ unsigned long long g_wave_times[2][kWtMax][3];
-struct WaveTimer {
-  int k;
-  unsigned long long t0;
-  __device__ explicit WaveTimer(int kk) : k(kk), t0(__builtin_amdgcn_s_memrealtime()) {}
-  __device__ ~WaveTimer() {
-    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0 && blockIdx.x < kWtMax) {
-      const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-      const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
-      g_wave_times[k][blockIdx.x][0] = t0;
-      g_wave_times[k][blockIdx.x][1] = t1;
-      g_wave_times[k][blockIdx.x][2] = ((unsigned long long)xcc << 32) | hw;
-    }
-  }
-};
-#define GS_WAVE_TIMER(k) WaveTimer wave_timer_(k)
-#else
-#define GS_WAVE_TIMER(k)
-#endif
 
 // torch.clamp semantics (NaN propagates)
 __device__ __forceinline__ float clamp01(float v) { return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
@@ -485,23 +455,13 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restric
     const long long idx = base + r * 64 + lane;
     kr[r] = keys[idx < n ? idx : n - 1];
   }
-#if GS_HIST_DIRECT_ATOMICS
-  // one LDS atomic per key (the LDS serialises equal addresses itself)
+  // one LDS atomic per key (the LDS serialises equal addresses itself;
+  // ballot-matched digit counts were 9 us slower on the tile sort)
 #pragma unroll
   for (int r = 0; r < kSortIpt; ++r) {
     const long long idx = base + r * 64 + lane;
     if (idx < n) atomicAdd(&hist[(kr[r] >> shift) & mask], 1u);
   }
-#else
-#pragma unroll
-  for (int r = 0; r < kSortIpt; ++r) {
-    const long long idx = base + r * 64 + lane;
-    const bool valid = idx < n;
-    const uint32_t d = valid ? ((kr[r] >> shift) & mask) : 0u;
-    const unsigned long long m = match_digit(d, nbits, __ballot(valid));
-    if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(m));
-  }
-#endif
   __syncthreads();
   if (threadIdx.x <= mask) counts[(size_t)threadIdx.x * nb + blockIdx.x] = hist[threadIdx.x];
 }
@@ -1108,9 +1068,6 @@ __device__ __forceinline__ float2 lds_pair(const float2 *p) {
 // s: |s_fp32 - s| <= ~4u (q00 dx^2 + |qo dx dy| + q11 dy^2) <= 4u (tr + |qo|)
 // tr / det * s, so conics with (tr + |qo|) tr > 1e4 det -- and
 // non-positive-definite or NaN ones -- are never culled.
-#ifndef GS_CELL_EXACT
-#define GS_CELL_EXACT 1
-#endif
 __device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo, float q11, float x0, float y0) {
   const float q01 = 0.5f * qo;
   const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
@@ -1120,7 +1077,6 @@ __device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo
   const float id = __builtin_amdgcn_rcpf(det);
   const float hx = __builtin_amdgcn_sqrtf(L * q11 * id), hy = __builtin_amdgcn_sqrtf(L * q00 * id);
   const bool box = mx + hx >= x0 && mx - hx <= x0 + 7.f && my + hy >= y0 && my - hy <= y0 + 7.f;
-#if GS_CELL_EXACT
   if (!box) return false;
   // The ellipse's bounding box meets the cell: the minimum of s over the
   // cell's box decides (a tilted, elongated ellipse's bounding box is much
@@ -1138,36 +1094,33 @@ __device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo
   const float e2 = sv(__builtin_amdgcn_fmed3f(ky * ay0, ax0, ax1), ay0);
   const float e3 = sv(__builtin_amdgcn_fmed3f(ky * ay1, ax0, ax1), ay1);
   return fminf(fminf(e0, e1), fminf(e2, e3)) <= L;
-#else
-  return box;
-#endif
 }
 
 // Workgroup b -> (tile, cell) and the tile's list range: b, b+8, b+16, ...
 // share an XCD (round-robin dispatch; placement is for speed only), so the Q
 // cells of a tile read its records through one L2.  Grid: ceil(tiles / 8) *
-// 8 Q.  Position (b / 8 / Q) * 8 + b % 8 is the tile itself, or, with a
-// dispatch order (gs_tile_order: the tiles with the most work first, so the
-// launch's last round is made of short workgroups), its entry (tile, start,
-// end) -- one load either way.  tile >= num_tiles: padding, no range.
-__device__ __forceinline__ void cell_tile(uint32_t b, int ncell, const uint32_t *order, const uint32_t *ranges,
-                                          int ntiles, int &tile, int &quad, uint32_t &start, uint32_t &end) {
+// 8 Q.  Position (b / 8 / Q) * 8 + b % 8 is the tile.  tile >= num_tiles:
+// padding, no range.  (A heaviest-first dispatch order saved 4-9 us per
+// launch at C3 but cost ~14 us to sort: tools/variants/README.md.)  The
+// range is clamped to the T list entries (scalar, free): a corrupt ranges
+// table cannot make the kernels read past sorted_gauss; a -DGS_DEBUG=1 build
+// also reports any range it had to clamp.
+__device__ __forceinline__ void cell_tile(uint32_t b, int ncell, const uint32_t *ranges, int ntiles, uint32_t T,
+                                          int &tile, int &quad, uint32_t &start, uint32_t &end) {
   const uint32_t grp = b >> 3;
   const uint32_t q = (uint32_t)ncell;
   quad = (int)(grp % q);
-  const uint32_t pos = (grp / q) * 8u + (b & 7u);
+  tile = (int)((grp / q) * 8u + (b & 7u));
   start = end = 0u;
-  if (order) {
-    const uint4 o = reinterpret_cast<const uint4 *>(order)[pos];
-    tile = (int)__builtin_amdgcn_readfirstlane(o.x);
-    start = __builtin_amdgcn_readfirstlane(o.y);
-    end = __builtin_amdgcn_readfirstlane(o.z);
-  } else {
-    tile = (int)pos;
-    if (tile < ntiles) {
-      start = __builtin_amdgcn_readfirstlane(ranges[2 * pos]);
-      end = __builtin_amdgcn_readfirstlane(ranges[2 * pos + 1]);
-    }
+  if (tile < ntiles) {
+    start = __builtin_amdgcn_readfirstlane(ranges[2 * tile]);
+    end = __builtin_amdgcn_readfirstlane(ranges[2 * tile + 1]);
+#if GS_DEBUG
+    if ((end > T || start > end) && threadIdx.x == 0)
+      printf("gsplat: tile %d range [%u, %u) outside the %u entries, clamped\n", tile, start, end, T);
+#endif
+    end = min(end, T);
+    start = min(start, end);
   }
 }
 
@@ -1193,13 +1146,12 @@ __device__ __forceinline__ void cell_tile(uint32_t b, int ncell, const uint32_t 
 // constants).
 template <bool kCount, bool kT16>
 __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
-  GS_WAVE_TIMER(0);
   __shared__ float2 s_rec[kWave * 6];
   const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
   const int ncell = cg.cells();
   int tile, quad;
   uint32_t start, end;
-  cell_tile(blockIdx.x, ncell, a.tile_order, a.ranges, a.tiles_x * a.tiles_y, tile, quad, start, end);
+  cell_tile(blockIdx.x, ncell, a.ranges, a.tiles_x * a.tiles_y, (uint32_t)a.num_pairs, tile, quad, start, end);
   if (tile >= a.tiles_x * a.tiles_y) return;
   const int lane = threadIdx.x;
   const int cx0 = (quad % cg.QX) * 8, cy0 = (quad / cg.QX) * 8;  // the cell in its tile
@@ -1218,7 +1170,6 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
   // evaluated entry (scalar), copied into a lane's neval only when it stops
   // (its bit leaves the running mask) -- two VALU less per evaluated entry
   uint32_t last = 0;
-  uint32_t work = 0;  // live (entry, cell) pairs: the backward's replay count
   unsigned long long runm = __builtin_amdgcn_ballot_w64(A < kAlphaStop);
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
@@ -1288,10 +1239,7 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
     }
     const uint64_t wi = (b - start) / 64u;
     if (lane == 0 && wi < live_left) live[wi] = livem;
-    work += (uint32_t)__builtin_popcountll(livem);
   }
-  // the entries the backward will replay in this cell: its dispatch-order key
-  if (a.cell_work && lane == 0) a.cell_work[(size_t)tile * ncell + quad] = work;
   if (!inside) return;
   if ((runm >> lane) & 1ull) neval = last;
   if (A < kAlphaStop) neval = end - start;
@@ -1305,124 +1253,6 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
   reinterpret_cast<float4 *>(a.pix_acc)[p] = make_float4(ar, ag, ab, D);
   reinterpret_cast<float2 *>(a.pix_state)[p] = make_float2(A, __uint_as_float(neval));
   if constexpr (kCount) a.pair_counts[p] = ncontrib;
-}
-
-// ================================================ blend dispatch order ====
-// The blend launches run ~4 rounds of workgroups per slot at C3, so the
-// launch ends with a round in which slots fall idle one by one; the longer
-// the workgroups still starting late, the longer that tail (measured with
-// per-workgroup clocks, tools/wave_times.py: residency averages 0.80 / 0.83
-// of its peak over the forward / backward launch).  k_tile_order lists the
-// tiles by expected work, largest first (a counting sort on 256 buckets of
-// key * 256 / (max + 1)), so the late starters are the short ones: the key is
-// the tile's list length before the forward, and the forward's per-cell
-// replay counts (cell_work, summed over the tile's cells) before the
-// backward.  Position p of the order is (tile, start, end, 0): the blend
-// workgroup reads its tile and list range in one load, as it read the range
-// before.  Only the dispatch order changes: every workgroup computes the same
-// outputs, so the order within a bucket (LDS atomics) is free.  Positions
-// past num_tiles (the grid's padding to 8) get tile = num_tiles, which the
-// blend kernels skip.  One 1024-thread workgroup; each thread holds 8 tiles'
-// keys (loads issued together) when num_tiles <= 8192, else re-reads them per
-// pass and chunk.
-constexpr int kOrdThreads = 1024, kOrdIpt = 8, kOrdChunk = kOrdThreads * kOrdIpt, kOrdBuckets = 256;
-// KIND 0: key = list length; 1: cell_work of 4 cells; 2: cell_work, any cells
-// (compile-time, so a thread's loads are issued together: under a runtime
-// branch each was waited for at its join, 16 us per launch)
-template <int KIND>
-__global__ __launch_bounds__(kOrdThreads) void k_tile_order(gs_order_args a) {
-  __shared__ uint32_t s_hist[kOrdBuckets];
-  __shared__ uint32_t s_max;
-  const int n = a.num_tiles, tid = threadIdx.x;
-  const int chunks = (n + kOrdChunk - 1) / kOrdChunk;
-  uint32_t key[kOrdIpt];
-  uint2 rg[kOrdIpt];
-  auto load = [&](int c) {
-#pragma unroll
-    for (int j = 0; j < kOrdIpt; ++j) {
-      const int t = c * kOrdChunk + j * kOrdThreads + tid;
-      const int tt = t < n ? t : 0;
-      rg[j] = reinterpret_cast<const uint2 *>(a.ranges)[tt];
-      uint32_t k;
-      if constexpr (KIND == 0) {
-        k = rg[j].y - rg[j].x;
-      } else if constexpr (KIND == 1) {
-        const uint4 w = reinterpret_cast<const uint4 *>(a.cell_work)[tt];
-        k = (w.x + w.y) + (w.z + w.w);
-      } else {
-        k = 0;
-        for (int q = 0; q < a.cells; ++q) k += a.cell_work[(size_t)tt * a.cells + q];
-      }
-      key[j] = t < n ? k : 0u;
-    }
-  };
-  if (tid == 0) s_max = 0;
-  if (tid < kOrdBuckets) s_hist[tid] = 0;
-  if (chunks == 1) load(0);
-  uint32_t m = 0;
-  for (int c = 0; c < chunks; ++c) {
-    if (chunks > 1) load(c);
-#pragma unroll
-    for (int j = 0; j < kOrdIpt; ++j) m = max(m, key[j]);
-  }
-  m = wave_max_u32(m);
-  __syncthreads();
-  if ((tid & (kWave - 1)) == 0) atomicMax(&s_max, m);
-  __syncthreads();
-  // (a float scale, not an integer division: a 64-bit divide is a long
-  // software sequence per key; any monotone bucket function will do)
-  const float scale = (float)kOrdBuckets / ((float)s_max + 1.f);
-  auto bucket = [&](uint32_t k) {
-    return (uint32_t)(kOrdBuckets - 1) - min((uint32_t)(kOrdBuckets - 1), (uint32_t)((float)k * scale));
-  };
-  // LDS atomics aggregated per wave: the lanes holding one bucket (ballot
-  // match) add once -- keys cluster in a few buckets, and same-address lanes
-  // of one atomic instruction serialise (11 us per launch unaggregated)
-  const unsigned long long lt = lanemask_lt();
-  for (int c = 0; c < chunks; ++c) {
-    if (chunks > 1) load(c);
-#pragma unroll
-    for (int j = 0; j < kOrdIpt; ++j) {
-      const bool valid = c * kOrdChunk + j * kOrdThreads + tid < n;
-      const uint32_t bk = bucket(key[j]);
-      const unsigned long long peers = match_digit(bk, 8, __ballot(valid));
-      if (valid && (peers & lt) == 0) atomicAdd(&s_hist[bk], (uint32_t)__popcll(peers));
-    }
-  }
-  __syncthreads();
-  if (tid < kWave) {  // exclusive scan of the 256 bucket counts: 4 per lane
-    uint32_t v[4], sum = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { v[i] = s_hist[4 * tid + i]; sum += v[i]; }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t t = __shfl_up(incl, d, kWave);
-      if (tid >= d) incl += t;
-    }
-    uint32_t run = incl - sum;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { s_hist[4 * tid + i] = run; run += v[i]; }
-  }
-  __syncthreads();
-  uint4 *out = reinterpret_cast<uint4 *>(a.tile_order);
-  for (int c = 0; c < chunks; ++c) {
-    if (chunks > 1) load(c);
-#pragma unroll
-    for (int j = 0; j < kOrdIpt; ++j) {
-      const int t = c * kOrdChunk + j * kOrdThreads + tid;
-      const bool valid = t < n;
-      const uint32_t bk = bucket(key[j]);
-      const unsigned long long peers = match_digit(bk, 8, __ballot(valid));
-      const uint32_t rank = (uint32_t)__popcll(peers & lt);
-      uint32_t base = 0;
-      if (valid && rank == 0) base = atomicAdd(&s_hist[bk], (uint32_t)__popcll(peers));
-      base = (uint32_t)__shfl((int)base, valid ? (int)__ffsll((long long)peers) - 1 : 0, kWave);
-      if (valid) out[base + rank] = make_uint4((uint32_t)t, rg[j].x, rg[j].y, 0u);
-    }
-  }
-  const int padded = (n + 7) & ~7;
-  for (int p = n + tid; p < padded; p += kOrdThreads) out[p] = make_uint4((uint32_t)n, 0u, 0u, 0u);
 }
 
 // ======================================================== blend bwd =======
@@ -1443,23 +1273,14 @@ __global__ __launch_bounds__(kOrdThreads) void k_tile_order(gs_order_args a) {
 //    10 gradient values and reduce them with 3 DPP steps.
 // The records of a 64-entry word's live entries are gathered lane-parallel
 // one word ahead (registers), staged in LDS and read back as broadcasts.
-#ifndef GS_BWD_GROUP
-#define GS_BWD_GROUP 8
-#endif
-#ifndef GS_BWD_CHUNK_STAGE
-#define GS_BWD_CHUNK_STAGE 1
-#endif
-#ifndef GS_BWD_RECENTER  // phase-B row moments about the row nearest each mean (numerics; 0 = about row 0)
-#define GS_BWD_RECENTER 1
-#endif
-constexpr int kBwdGroup = GS_BWD_GROUP;  // live entries per phase-B group: 8 or 4
-static_assert(kBwdGroup == 8 || kBwdGroup == 4, "phase B maps 8 or 16 lanes to an entry");
-constexpr int kBwdLanes = kWave / kBwdGroup;  // lanes per entry in phase B (8 or 16)
-constexpr int kBwdStep = kBwdLanes / 8;       // row step of a lane's pixels (1 or 2)
+// live entries per phase-B group: 8, lanes 8j .. 8j + 7 on entry j (4 groups
+// of 16 lanes: +85 us, tools/variants/README.md)
+constexpr int kBwdGroup = 8;
+constexpr int kBwdLanes = kWave / kBwdGroup;  // lanes per entry in phase B
 // Group buffer rows (dop, c) are padded to 72 float2: phase B's lanes 8j + x
 // read row j at pixel x + 8r, and 72 puts rows j = 0..3 of a 32-lane half on
 // distinct banks (a stride of 64 would be a 4-way conflict).
-constexpr int kBwdRow = kBwdGroup == 8 ? kWave + 8 : kWave + 16;
+constexpr int kBwdRow = kWave + 8;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
@@ -1468,14 +1289,6 @@ __device__ __forceinline__ float dpp_row(float v) {
   // compiler fold the move into the add (v_add_f32_dpp); without it the
   // row_half_mirror step became v_mov 0 + v_mov_dpp + v_add
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
-}
-// Sum over the 16 lanes of each DPP row; every lane of the row gets the sum.
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_row<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_row<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_row<0x124>(v);  // row_ror:4
-  v += dpp_row<0x128>(v);  // row_ror:8
-  return v;
 }
 // Sum over the 8 lanes 8j..8j+7 (a DPP half row); each of them gets the sum.
 __device__ __forceinline__ float oct_sum(float v) {
@@ -1502,21 +1315,16 @@ __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
 
 template <bool kT16>
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
-  GS_WAVE_TIMER(1);
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
-#if GS_BWD_CHUNK_STAGE
   // the chunk's records (word 10 = slot), staged per chunk from registers:
   // 384 B instead of a word's 3 KB, for occupancy (LDS bounds it)
   __shared__ float2 s_wrec[kBwdGroup * 6];
-#else
-  __shared__ float2 s_wrec[kWave * 6];   // the word's live records, packed in bit order; word 10 = slot
-#endif
   const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
   const int ncell = cg.cells();
   int tile, quad;
   uint32_t start, lend;
-  cell_tile(blockIdx.x, ncell, a.tile_order, a.ranges, a.tiles_x * a.tiles_y, tile, quad, start, lend);
+  cell_tile(blockIdx.x, ncell, a.ranges, a.tiles_x * a.tiles_y, (uint32_t)a.num_pairs, tile, quad, start, lend);
   if (tile >= a.tiles_x * a.tiles_y) return;
   const int lane = threadIdx.x;
   const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
@@ -1602,15 +1410,15 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       r2 = recs[3 * (size_t)gid + 2];
     }
   };
-  // Phase B over a chunk: the k live entries of the current word staged at
-  // packed positions kb .. kb + k - 1 (group order).
-  auto phase_b = [&](auto masked_tag, uint32_t kb, int k) {
+  // Phase B over a chunk: its k live entries, staged at s_wrec positions
+  // 0 .. k - 1 (group order).
+  auto phase_b = [&](auto masked_tag, int k) {
     constexpr bool kMasked = decltype(masked_tag)::value;
     // (the group buffer rows were written by this wave: waited for below)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int j = lane / kBwdLanes, sub = lane % kBwdLanes, col = sub & 7, row0 = sub >> 3;
+    const int j = lane / kBwdLanes, col = lane % kBwdLanes;
     if (j < k) {
-      const uint32_t e = (GS_BWD_CHUNK_STAGE ? 0u : kb) + (uint32_t)j;
+      const uint32_t e = (uint32_t)j;
       const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * e];  // mx my q00 q11
       const float2 ib = s_wrec[6 * e + 2];                                // qo o
       const uint32_t slot = __float_as_uint(s_wrec[6 * e + 5].x);
@@ -1631,44 +1439,49 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       auto moments = [&](auto recenter_tag) {
         constexpr bool kRec = decltype(recenter_tag)::value;
         if constexpr (kRec)
-          rc = __builtin_amdgcn_fmed3f(__builtin_rintf((ia.y - (float)(y0 + row0)) * (1.f / kBwdStep)), 0.f,
-                                       (float)(kBwdGroup - 1)) * kBwdStep;
+          rc = __builtin_amdgcn_fmed3f(__builtin_rintf(ia.y - (float)y0), 0.f, (float)(kBwdGroup - 1));
 #pragma unroll
         for (int r = 0; r < kBwdGroup; ++r) {
-          const int p = col + 8 * (row0 + kBwdStep * r);  // phase A's lane of that pixel
+          const int p = col + 8 * r;  // phase A's lane of that pixel
           const float2 dc = s_dc[j][p];
           const float dop = dc.x, cs = dc.y;
           const float4 pg = s_pg[p];
-          // dL/ds: none where the weight clamp bound (sign bit of c) or the pair
-          // was skipped (dop = 0 then); a simple entry's clamps never bind
-          const float ds = kMasked ? (cs > 0.f ? hop * dop : 0.f) : hop * dop;
+          // dL/ds = hop dop: none where the weight clamp bound (sign bit of c)
+          // or the pair was skipped (dop = 0 then); a simple entry's clamps
+          // never bind.  The moments are summed over dop and scaled by the
+          // entry's hop once, after the rows (2 VALU less per row; unmasked,
+          // the opacity sum g5 is the moment S0 itself)
+          const float ds = kMasked ? (cs > 0.f ? dop : 0.f) : dop;
           const float cw = fabsf(cs);
           S0 += ds;
           if constexpr (kRec) {
-            const float w = (float)(kBwdStep * r) - rc;  // exact: small integers
+            const float w = (float)r - rc;  // exact: small integers
             Soy = __builtin_fmaf(ds, w, Soy);
             Soyy = __builtin_fmaf(ds, w * w, Soyy);
           } else if (r) {
-            Soy = __builtin_fmaf(ds, (float)(kBwdStep * r), Soy);
-            Soyy = __builtin_fmaf(ds, (float)(kBwdStep * kBwdStep * r * r), Soyy);
+            Soy = __builtin_fmaf(ds, (float)r, Soy);
+            Soyy = __builtin_fmaf(ds, (float)(r * r), Soyy);
           }
-          g5 += dop;
+          if constexpr (kMasked) g5 += dop;
           g6 = __builtin_fmaf(pg.x, cw, g6);
           g7 = __builtin_fmaf(pg.y, cw, g7);
           g8 = __builtin_fmaf(pg.z, cw, g8);
           g9 = __builtin_fmaf(pg.w, cw, g9);
         }
       };
-      if (GS_BWD_RECENTER && wave_any(small_y)) moments(std::true_type{}); else moments(std::false_type{});
-      const float by = (float)(y0 + row0) + rc - ia.y;
+      if (wave_any(small_y)) moments(std::true_type{}); else moments(std::false_type{});
+      if constexpr (!kMasked) g5 = S0;
+      S0 *= hop;
+      Soy *= hop;
+      Soyy *= hop;
+      const float by = (float)y0 + rc - ia.y;
       // sums of ds dx, ds dy, ds dx^2, ds dx dy, ds dy^2 over the lane's column
       float Sx = bx * S0, Sy = __builtin_fmaf(by, S0, Soy);
       float g2 = bx * Sx, g3 = bx * Sy;
       float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
-      auto red = [](float v) { return kBwdLanes == 8 ? oct_sum(v) : row16_sum(v); };
-      Sx = red(Sx); Sy = red(Sy); g2 = red(g2); g3 = red(g3); g4 = red(g4);
-      g5 = red(g5); g6 = red(g6); g7 = red(g7); g8 = red(g8); g9 = red(g9);
-      if (sub == 0) {
+      Sx = oct_sum(Sx); Sy = oct_sum(Sy); g2 = oct_sum(g2); g3 = oct_sum(g3); g4 = oct_sum(g4);
+      g5 = oct_sum(g5); g6 = oct_sum(g6); g7 = oct_sum(g7); g8 = oct_sum(g8); g9 = oct_sum(g9);
+      if (col == 0) {
         const float q00 = ia.z, qo = ib.x, q11 = ia.w;
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
@@ -1694,24 +1507,13 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     // chunk's records sit at compile-time offsets from one base address
     const uint32_t rank =
         __builtin_amdgcn_mbcnt_hi((uint32_t)(mcur >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mcur, 0u));
-#if GS_BWD_CHUNK_STAGE
     // this word's records stay in registers (staged chunk by chunk below)
-    // while the next word's are fetched into r0..r2
+    // while the next word's are fetched into r0..r2 (staging a whole word's
+    // records, 3 KB of LDS, cost occupancy: -13 us when chunked)
     const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
-#else
-    if (mine) {
-      float4 *d = reinterpret_cast<float4 *>(&s_wrec[6 * rank]);
-      d[0] = r0;
-      d[1] = r1;
-      d[2] = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
-    }
-#endif
     const unsigned long long simple_w = __builtin_amdgcn_ballot_w64(mine && simple_entry(r0, r1));
     const unsigned long long mnext = wd + 1u < nwords ? live_word(wd + 1u) : 0ull;
     fetch(wd + 1u, mnext);  // in flight while this word replays
-#if !GS_BWD_CHUNK_STAGE
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
-#endif
     // a word whose live entries are all simple (the common case) runs a copy
     // of the loop without the per-entry test
     auto run_word = [&](auto all_simple_tag) {
@@ -1722,7 +1524,6 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
      // a chunk: the word's next (up to) kBwdGroup live entries
      unsigned long long cm = 0;
      int k = 0;
-#if GS_BWD_CHUNK_STAGE
      // stage the chunk (ranks kb .. kb + kBwdGroup - 1; the previous chunk's
      // reads came before these writes in this wave's in-order LDS queue)
      if (mine && rank - kb < (uint32_t)kBwdGroup) {
@@ -1733,14 +1534,6 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
      }
      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
      const char *cb = reinterpret_cast<const char *>(s_wrec);
-#else
-     // the chunk's records: one VGPR base (asm: the compiler would otherwise
-     // re-materialise it from the SGPR with a v_mov per entry), entry kk at a
-     // compile-time offset from it
-     uint32_t vb;
-     asm volatile("v_mov_b32 %0, %1" : "=v"(vb) : "s"(kb * 48u));
-     const char *cb = reinterpret_cast<const char *>(s_wrec) + vb;
-#endif
      // unrolled: the group row k is a compile-time LDS offset
 #pragma unroll
      for (int kk = 0; kk < kBwdGroup; ++kk) {
@@ -1811,333 +1604,12 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       s_dc[kk][lane] = make_float2(dop, cw);
       k = kk + 1;
      }
-     if (kAllSimple || (simple_w & cm) == cm) phase_b(std::false_type{}, kb, k); else phase_b(std::true_type{}, kb, k);
+     if (kAllSimple || (simple_w & cm) == cm) phase_b(std::false_type{}, k); else phase_b(std::true_type{}, k);
      kb += (uint32_t)k;
     }
     };
     if ((simple_w & mcur) == mcur) run_word(std::true_type{}); else run_word(std::false_type{});
     mcur = mnext;
-  }
-}
-
-// ============================================ blend bwd, combined cells ===
-// The default 16x16 tile: one wave takes kBwdCpw of the tile's four 8x8
-// cells (4: the whole tile, 2: a 16x8 half) and replays them word by word --
-// for each 64-entry word of the tile's list, its cells in turn, each over its
-// own liveness bits with its own pixel chains exactly as k_blend_bwd does
-// for one cell -- and adds the cells' phase-B sums of an entry in registers
-// (lane = the entry's bit in the word, cells in a fixed order) before
-// anything leaves the chip: one partial per (entry, group of kBwdCpw cells)
-// instead of one per (entry, cell), so the partial stores and the gather's
-// reads shrink by the cells an entry reaches on average (2.6 at C3).  A
-// cell's per-pixel state rotates through cs[0]: the per-cell body is not
-// unrolled (code size), the rotation costs a few moves per (word, cell).
-#ifndef GS_BWD_CPW
-#define GS_BWD_CPW 1
-#endif
-constexpr int kBwdCpw = GS_BWD_CPW;
-static_assert(kBwdCpw == 1 || kBwdCpw == 2 || kBwdCpw == 4, "cells per backward wave: 1, 2 or 4");
-
-// One pixel's backward state in one cell.
-struct BwdPixel {
-  float gR0, gR1, gR2, gD, gA;  // cotangents through clamp / bg composite / depth normalisation
-  float A, T1, PG;              // the replay: A, 1 - A (carried), P + G0 (see k_blend_bwd)
-  uint32_t neval;               // entries the forward evaluated for this pixel
-};
-
-template <int CPW>
-__global__ __launch_bounds__(kWave) void k_blend_bwd_grp(gs_blend_bwd_args a) {
-  __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
-  __shared__ float4 s_pg[kWave];               // the current cell's pixels: dL/drgb (masked), dL/dD
-  __shared__ float2 s_wrec[kBwdGroup * 6];     // the chunk's records (word 10 = slot)
-  constexpr int NG = 4 / CPW;                  // partial groups per tile
-  const int ntiles = a.tiles_x * a.tiles_y;
-  // workgroup b -> (tile, group): the XCD b & 7 (round-robin dispatch) takes
-  // the row-major band of tiles [x per, (x + 1) per), so neighbouring tiles,
-  // which share Gaussians, read records through one L2 (speed only)
-  const uint32_t per = ((uint32_t)ntiles + 7u) >> 3, kq = blockIdx.x >> 3;
-  const int grp = (int)(kq % (uint32_t)NG);
-  const int tile = (int)((blockIdx.x & 7u) * per + kq / (uint32_t)NG);
-  if (tile >= ntiles) return;
-  const int lane = threadIdx.x;
-  const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
-  const uint32_t start = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile]);
-  const uint32_t lend = __builtin_amdgcn_readfirstlane(a.ranges[2 * tile + 1]);
-  if (start >= lend) return;
-  const float4 *recs = reinterpret_cast<const float4 *>(a.records);
-  const int W = a.cam.image_width, H = a.cam.image_height;
-  const size_t HW = (size_t)W * H;
-  const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
-  // the prologue's loads in two round trips, unconditionally (k_blend_bwd):
-  // every cell's pixel state and cotangents and word-0 liveness word, the
-  // word-0 entries' ids; then speculatively every word-0 entry's record
-  const unsigned long long *lwb = reinterpret_cast<const unsigned long long *>(a.live_bits);
-  const size_t lw_off = start / 64u + (uint32_t)tile;
-  unsigned long long w0[CPW];
-  float4 accp[CPW];
-  float2 stp[CPW];
-  float gip[CPW][5];
-  bool inside[CPW];
-#pragma unroll
-  for (int i = 0; i < CPW; ++i) {
-    const int c = grp * CPW + i;
-    const int px = (int)tx * 16 + (c & 1) * 8 + (lane & 7), py = (int)ty * 16 + (c >> 1) * 8 + (lane >> 3);
-    inside[i] = px < W && py < H;
-    const size_t p = inside[i] ? (size_t)py * W + px : 0;
-    w0[i] = lwb[(size_t)c * a.live_words + lw_off];
-    accp[i] = reinterpret_cast<const float4 *>(a.pix_acc)[p];
-    stp[i] = reinterpret_cast<const float2 *>(a.pix_state)[p];
-    gip[i][0] = a.g_image[p];
-    gip[i][1] = a.g_image[HW + p];
-    gip[i][2] = a.g_image[2 * HW + p];
-    gip[i][3] = (a.g_alpha ? a.g_alpha : a.g_image)[p];
-    gip[i][4] = (a.g_depth ? a.g_depth : a.g_image)[p];
-  }
-  const uint32_t gid0 = a.sorted_gauss[start + (uint32_t)lane < lend ? start + (uint32_t)lane : 0u];
-  float4 r0 = recs[3 * (size_t)gid0], r1 = recs[3 * (size_t)gid0 + 1], r2 = recs[3 * (size_t)gid0 + 2];
-  BwdPixel cs[CPW];
-  uint32_t nwords[CPW], wstop[CPW];
-  uint32_t nw = 0;
-#pragma unroll
-  for (int i = 0; i < CPW; ++i) {
-    // pixel cotangents (k_blend_bwd; selects, no branch)
-    const bool in = inside[i];
-    const float tr = in ? accp[i].x : 0.f, tg = in ? accp[i].y : 0.f, tbl = in ? accp[i].z : 0.f;
-    const float Dt = in ? accp[i].w : 0.f, At = in ? stp[i].x : 0.f;
-    const float tb = 1.f - At;
-    const float pr = tr + tb * bg0, pg = tg + tb * bg1, pb = tbl + tb * bg2;
-    BwdPixel &P = cs[i];
-    P.gR0 = (in && pr >= 0.f && pr <= 1.f) ? gip[i][0] : 0.f;
-    P.gR1 = (in && pg >= 0.f && pg <= 1.f) ? gip[i][1] : 0.f;
-    P.gR2 = (in && pb >= 0.f && pb <= 1.f) ? gip[i][2] : 0.f;
-    float gA = -P.gR0 * bg0 - P.gR1 * bg1 - P.gR2 * bg2;
-    if (in && a.g_alpha && At >= 0.f && At <= 1.f) gA += gip[i][3];
-    const bool has_d = in && a.g_depth;
-    const float den = At + 1e-6f;
-    P.gD = has_d ? gip[i][4] / den : 0.f;
-    const float gAd = -gip[i][4] * Dt / (den * den);
-    if (has_d) gA += gAd;
-    P.gA = gA;
-    P.neval = in ? __float_as_uint(stp[i].y) : 0u;
-    const float K = (P.gR0 * tr + P.gR1 * tg) + (P.gR2 * tbl + P.gD * Dt);
-    const float G0 = __builtin_fmaf(gA, 1.f - At, -K);
-    P.PG = ((P.gR0 * bg0 + P.gR1 * bg1) + P.gR2 * bg2) + G0;
-    P.A = 0.f;
-    P.T1 = 1.f;
-    wstop[i] = __builtin_amdgcn_readfirstlane(wave_max_u32(P.neval));
-    nwords[i] = (wstop[i] + 63u) >> 6;
-    nw = nw > nwords[i] ? nw : nwords[i];
-  }
-  if (nw == 0) return;
-  // liveness word wd of cell i, cut at the cell's last evaluated entry (bits
-  // past it were never written; words past it are not read)
-  auto live_word = [&](int i, uint32_t wd) -> unsigned long long {
-    if (wd >= nwords[i]) return 0ull;
-    const unsigned long long w = wd == 0 ? w0[i] : lwb[(size_t)(grp * CPW + i) * a.live_words + lw_off + wd];
-    const unsigned long long m =
-        ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32) |
-        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)w);
-    const uint32_t rem = wstop[i] - 64u * wd;
-    return rem < 64u ? m & ((1ull << rem) - 1ull) : m;
-  };
-  unsigned long long mc[CPW];
-#pragma unroll
-  for (int i = 0; i < CPW; ++i) mc[i] = live_word(i, 0);
-  const int j = lane / kBwdLanes, sub = lane % kBwdLanes, col = sub & 7, row0 = sub >> 3;
-  for (uint32_t wd = 0; wd < nw; ++wd) {
-    unsigned long long U = 0;
-#pragma unroll
-    for (int i = 0; i < CPW; ++i) U |= mc[i];
-    const bool mineU = (U >> lane) & 1ull;
-    // word 10 of a live record becomes the entry's gradient slot
-    const uint32_t info = __float_as_uint(r2.w);
-    const uint32_t slot = __float_as_uint(r2.z) + (ty - ((info >> 12) & 0xFFFu)) * ((info >> 24) + 1u) +
-                          (tx - (info & 0xFFFu));
-    const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
-    const unsigned long long simple_w = __builtin_amdgcn_ballot_w64(mineU && simple_entry(r0, r1));
-    unsigned long long mn[CPW], Un = 0;
-#pragma unroll
-    for (int i = 0; i < CPW; ++i) {
-      mn[i] = live_word(i, wd + 1u);
-      Un |= mn[i];
-    }
-    if ((Un >> lane) & 1ull) {  // the next word's records, in flight while this word replays
-      const uint32_t gid = a.sorted_gauss[start + 64u * (wd + 1u) + (uint32_t)lane];
-      r0 = recs[3 * (size_t)gid];
-      r1 = recs[3 * (size_t)gid + 1];
-      r2 = recs[3 * (size_t)gid + 2];
-    }
-    // this word's entries' partials summed over the cells; lane = entry bit
-    float acc[GS_PAIR_GRAD_FLOATS];
-#pragma unroll
-    for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
-#pragma unroll 1
-    for (int i = 0; i < CPW; ++i) {
-      const unsigned long long mcell = mc[0];
-      if (mcell) {
-        BwdPixel &P = cs[0];
-        const int c = grp * CPW + i;
-        const int x0 = (int)tx * 16 + (c & 1) * 8, y0 = (int)ty * 16 + (c >> 1) * 8;
-        const float fx = (float)(x0 + (lane & 7)), fy = (float)(y0 + (lane >> 3));
-        // (the previous cell's phase-B reads precede this write in the wave's LDS queue)
-        s_pg[lane] = make_float4(P.gR0, P.gR1, P.gR2, P.gD);
-        const bool mine = (mcell >> lane) & 1ull;
-        const uint32_t rank =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(mcell >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mcell, 0u));
-        // Phase B over a chunk of k live entries (k_blend_bwd), the sums then
-        // moved to the lanes of their word bits and added to acc
-        auto phase_b = [&](auto masked_tag, unsigned long long cm, int k) {
-          constexpr bool kMasked = decltype(masked_tag)::value;
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the group buffer rows
-          float v[GS_PAIR_GRAD_FLOATS];
-#pragma unroll
-          for (int q = 0; q < GS_PAIR_GRAD_FLOATS; ++q) v[q] = 0.f;
-          if (j < k) {
-            const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * j];  // mx my q00 q11
-            const float2 ib = s_wrec[6 * j + 2];                                // qo o
-            const float hop = -0.5f * ib.y;
-            const float bx = (float)(x0 + col) - ia.x;  // (row moments about rc: k_blend_bwd)
-            const float rc = GS_BWD_RECENTER ? __builtin_amdgcn_fmed3f(__builtin_rintf((ia.y - (float)(y0 + row0)) *
-                                                                                        (1.f / kBwdStep)),
-                                                                       0.f, (float)(kBwdGroup - 1)) * kBwdStep
-                                             : 0.f;
-            const float by = (float)(y0 + row0) + rc - ia.y;
-            float S0 = 0.f, Soy = 0.f, Soyy = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
-#pragma unroll
-            for (int r = 0; r < kBwdGroup; ++r) {
-              const int p = col + 8 * (row0 + kBwdStep * r);
-              const float2 dc = s_dc[j][p];
-              const float dop = dc.x, csg = dc.y;
-              const float4 pg = s_pg[p];
-              const float ds = kMasked ? (csg > 0.f ? hop * dop : 0.f) : hop * dop;
-              const float cw = fabsf(csg);
-              S0 += ds;
-              const float w = (float)(kBwdStep * r) - rc;
-              Soy = __builtin_fmaf(ds, w, Soy);
-              Soyy = __builtin_fmaf(ds, w * w, Soyy);
-              g5 += dop;
-              g6 = __builtin_fmaf(pg.x, cw, g6);
-              g7 = __builtin_fmaf(pg.y, cw, g7);
-              g8 = __builtin_fmaf(pg.z, cw, g8);
-              g9 = __builtin_fmaf(pg.w, cw, g9);
-            }
-            float Sx = bx * S0, Sy = __builtin_fmaf(by, S0, Soy);
-            float g2 = bx * Sx, g3 = bx * Sy;
-            float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
-            auto red = [](float x) { return kBwdLanes == 8 ? oct_sum(x) : row16_sum(x); };
-            Sx = red(Sx); Sy = red(Sy); g2 = red(g2); g3 = red(g3); g4 = red(g4);
-            g5 = red(g5); g6 = red(g6); g7 = red(g7); g8 = red(g8); g9 = red(g9);
-            const float q00 = ia.z, qo = ib.x, q11 = ia.w;
-            v[0] = -(2.f * q00 * Sx + qo * Sy);
-            v[1] = -(qo * Sx + 2.f * q11 * Sy);
-            v[2] = g2; v[3] = g3; v[4] = g4; v[5] = g5; v[6] = g6; v[7] = g7; v[8] = g8; v[9] = g9;
-          }
-          // lane L of the chunk's bit set takes the sums of chunk entry
-          // rank(L) from lane rank(L) * kBwdLanes
-          const uint32_t jr =
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-          const int src = (int)(jr * (uint32_t)kBwdLanes) << 2;
-          const bool take = (cm >> lane) & 1ull;
-#pragma unroll
-          for (int q = 0; q < GS_PAIR_GRAD_FLOATS; ++q) {
-            const float t = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v[q])));
-            acc[q] += take ? t : 0.f;
-          }
-        };
-        auto run_word = [&](auto all_simple_tag) {
-          constexpr bool kAllSimple = decltype(all_simple_tag)::value;
-          unsigned long long m = mcell;
-          uint32_t kb = 0;
-          while (m) {
-            unsigned long long cm = 0;
-            int k = 0;
-            if (mine && rank - kb < (uint32_t)kBwdGroup) {
-              float4 *d = reinterpret_cast<float4 *>(&s_wrec[6 * (rank - kb)]);
-              d[0] = c0;
-              d[1] = c1;
-              d[2] = c2;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
-            const char *cb = reinterpret_cast<const char *>(s_wrec);
-#pragma unroll
-            for (int kk = 0; kk < kBwdGroup; ++kk) {
-              if (kk > 0 && !m) break;
-              const uint32_t bit = (uint32_t)__builtin_ctzll(m);
-              m &= m - 1ull;
-              cm |= 1ull << bit;
-              const uint32_t ie = 64u * wd + bit;
-              const float4 r0v = reinterpret_cast<const float4 *>(cb + 48 * kk)[0];
-              const float4 r1v = reinterpret_cast<const float4 *>(cb + 48 * kk)[1];
-              const float2 pbz = reinterpret_cast<const float2 *>(cb + 48 * kk)[4];
-              const float dx = fx - r0v.x, dy = fy - r0v.y;
-              const float sq = conic_s(dx, dy, r0v.z, r1v.x, r0v.w);
-              const bool live = (ie < P.neval) && !(sq > kSkipS);
-              const float X = __builtin_fmaf(P.gR0, r1v.z,
-                                             __builtin_fmaf(P.gR1, r1v.w, __builtin_fmaf(P.gR2, pbz.x, P.gD * pbz.y)));
-              const bool simple = kAllSimple || ((simple_w >> bit) & 1ull);
-              float dop, cw;
-              if (simple) {
-                const float w = exp_neg_half(sq);
-                const float wv = live ? w : 0.f;
-                const float trans = P.T1;
-                const float c = trans * (r1v.y * wv);
-                P.A = P.A + c;
-                P.PG = __builtin_fmaf(c, X, P.PG);
-                P.T1 = 1.f - P.A;
-                const float inv = __builtin_amdgcn_rcpf(P.T1);
-                const float d_live = __builtin_fmaf(inv, P.PG, X);
-                const float dal = trans * (P.A >= kAlphaStop ? X + P.gA : d_live);
-                dop = dal * wv;
-                cw = c;
-              } else {
-                const float e = exp_inrange(-0.5f * sq);
-                const float w = sat01(e);
-                const float u = r1v.y * w;
-                const float ai = sat01(u);
-                const float trans = P.T1;
-                const float c = trans * (live ? ai : 0.f);
-                P.A = P.A + c;
-                P.PG = __builtin_fmaf(c, X, P.PG);
-                const bool term = P.A >= kAlphaStop;
-                P.T1 = 1.f - P.A;
-                const float inv = __builtin_amdgcn_rcpf(P.T1);
-                const float d_live = __builtin_fmaf(inv, P.PG, X);
-                const float dal = trans * (term ? X + P.gA : d_live);
-                const float g = (ai == u) ? dal * w : 0.f;
-                dop = (c > 0.f) ? g : 0.f;
-                cw = (w == e) ? c : -c;
-              }
-              s_dc[kk][lane] = make_float2(dop, cw);
-              k = kk + 1;
-            }
-            if (kAllSimple || (simple_w & cm) == cm) phase_b(std::false_type{}, cm, k); else phase_b(std::true_type{}, cm, k);
-            kb += (uint32_t)k;
-          }
-        };
-        if ((simple_w & mcell) == mcell) run_word(std::true_type{}); else run_word(std::false_type{});
-      }
-      // rotate: the next cell's state into cs[0] (a full cycle restores the order)
-      const BwdPixel t = cs[0];
-      const unsigned long long tm = mc[0];
-#pragma unroll
-      for (int q = 0; q + 1 < CPW; ++q) {
-        cs[q] = cs[q + 1];
-        mc[q] = mc[q + 1];
-      }
-      cs[CPW - 1] = t;
-      mc[CPW - 1] = tm;
-    }
-    // one partial per (entry, group): lanes of entries any of the cells replayed
-    if (mineU) {
-      const size_t sq = (size_t)slot * NG + (uint32_t)grp;
-      float *out = a.pair_grads + sq * GS_PARTIAL_STRIDE;
-      *reinterpret_cast<f4_u8 *>(out) = f4_u8{acc[0], acc[1], acc[2], acc[3]};
-      *reinterpret_cast<f4_u8 *>(out + 4) = f4_u8{acc[4], acc[5], acc[6], acc[7]};
-      *reinterpret_cast<f2_u8 *>(out + 8) = f2_u8{acc[8], acc[9]};
-      a.slot_live[sq] = 1;
-    }
-#pragma unroll
-    for (int i = 0; i < CPW; ++i) mc[i] = mn[i];
   }
 }
 
@@ -2176,15 +1648,15 @@ __device__ __forceinline__ float lanes_sum(float v) {
 
 constexpr int kGatherHL1 = GS_GATHER_HL1;  // slot lanes per Gaussian with one partial group per slot
 
-template <int QL, int HL, int kNG = 0>  // kNG > 0: the partial groups per slot at compile time (else ng)
-__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng_rt) {
-  const uint32_t ng = kNG > 0 ? (uint32_t)kNG : ng_rt;
+constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
+
+// Gaussian g's partials summed by its QL x HL lanes (lane (h, q) of g at
+// t % LPG); every one of the LPG lanes returns the sum in acc.
+template <int QL, int HL, int kNG>
+__device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint32_t ng, long long t, float2 acc[kF2]) {
   constexpr int LPG = QL * HL;
   static_assert(LPG == 2 || LPG == 4 || LPG == 8, "lanes per Gaussian");
-  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const int g = (int)(t / LPG), h = (int)((t % LPG) / QL), q = (int)(t % QL);
-  constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
-  float2 acc[kF2];
 #pragma unroll
   for (int k = 0; k < kF2; ++k) acc[k] = make_float2(0.f, 0.f);
   // vis, rect and first slot in one round trip (the empty asm keeps the
@@ -2247,6 +1719,15 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, 
     acc[k].x = lanes_sum<LPG>(acc[k].x);
     acc[k].y = lanes_sum<LPG>(acc[k].y);
   }
+}
+
+template <int QL, int HL, int kNG = 0>  // kNG > 0: the partial groups per slot at compile time (else ng)
+__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng_rt) {
+  constexpr int LPG = QL * HL;
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int g = (int)(t / LPG);
+  float2 acc[kF2];
+  gather_slots<QL, HL, kNG>(a, kNG > 0 ? (uint32_t)kNG : ng_rt, t, acc);
   if ((t % LPG) == 0 && g < a.g.n) {
     float2 *out = reinterpret_cast<float2 *>(a.grad_sums) + (size_t)g * kF2;
 #pragma unroll
@@ -2254,16 +1735,10 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, 
   }
 }
 
-// kHot: partials present, no viewspace/conic cotangents, raw scale/rotation,
-// DC colour -- the training configuration.  Its loads are all issued up
-// front (a load under a runtime branch is waited for at the branch's join,
-// which serialised six round trips per thread in the generic instantiation).
-template <bool kHot>
-__global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
-  const int k = blockIdx.x * kBlock + threadIdx.x;
-  if (k >= a.g.n) return;
-  // in depth order, consecutive threads own adjacent slot ranges
-  const int g = (!kHot && a.order) ? (int)a.order[k] : k;
+// Gaussian g's chain rule from its summed blend gradients: sums(acc) fills
+// acc[10] (from k_gather_slots' [n, 10] sums, or the fused gather's LDS)
+template <bool kHot, typename Sums>
+__device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, int g, Sums sums) {
   float scl_pre[3] = {0.f, 0.f, 0.f}, rot_pre[4] = {0.f, 0.f, 0.f, 0.f}, op_pre = 0.f;
   if constexpr (kHot) {
 #pragma unroll
@@ -2274,17 +1749,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   }
   const float4 Qf = reinterpret_cast<const float4 *>(a.conics)[g];
   float acc[GS_PAIR_GRAD_FLOATS];
-#pragma unroll
-  for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
-  if (kHot || a.pair_grads) {  // g's partials summed (k_gather_slots)
-    const float2 *gs = reinterpret_cast<const float2 *>(a.grad_sums) + (size_t)g * (GS_PAIR_GRAD_FLOATS / 2);
-#pragma unroll
-    for (int k = 0; k < GS_PAIR_GRAD_FLOATS / 2; ++k) {
-      const float2 v = gs[k];
-      acc[2 * k] = v.x;
-      acc[2 * k + 1] = v.y;
-    }
-  }
+  sums(acc);
   float dm0 = acc[0], dm1 = acc[1];
   float G[4] = {acc[2], acc[3], acc[3], acc[4]};
   if (!kHot && a.g_means2d) {
@@ -2484,6 +1949,78 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   a.d_rotation[4 * (size_t)g + 3] = (dz - z * dot) * iq;
 }
 
+// kHot: partials present, no viewspace/conic cotangents, raw scale/rotation,
+// DC colour -- the training configuration.  Its loads are all issued up
+// front (a load under a runtime branch is waited for at the branch's join,
+// which serialised six round trips per thread in the generic instantiation).
+template <bool kHot>
+__global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
+  const int k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= a.g.n) return;
+  // in depth order, consecutive threads own adjacent slot ranges
+  const int g = (!kHot && a.order) ? (int)a.order[k] : k;
+  project_bwd_one<kHot>(a, g, [&](float acc[GS_PAIR_GRAD_FLOATS]) {
+#pragma unroll
+    for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
+    if (kHot || a.pair_grads) {  // g's partials summed (k_gather_slots)
+      const float2 *gs = reinterpret_cast<const float2 *>(a.grad_sums) + (size_t)g * kF2;
+#pragma unroll
+      for (int k = 0; k < kF2; ++k) {
+        const float2 v = gs[k];
+        acc[2 * k] = v.x;
+        acc[2 * k + 1] = v.y;
+      }
+    }
+  });
+}
+
+// The training configuration at the default tile (four partial groups per
+// slot), gather and chain rule in one launch: the workgroup's 256 Gaussians'
+// partials are summed 32 Gaussians per round (8 lanes each, as
+// k_gather_slots<4, 2, 4>, the same fixed order: bit-identical sums) into
+// LDS, then thread t runs Gaussian t's chain rule from there -- the [n, 10]
+// sums never reach HBM (40 B written + 40 B read per Gaussian) and one launch
+// goes.  Rows padded to 11 floats (bank spread of the per-thread reads).
+#ifndef GS_FUSED_GATHER
+#define GS_FUSED_GATHER 1
+#endif
+#ifndef GS_FUSED_UNROLL
+#define GS_FUSED_UNROLL 1
+#endif
+constexpr int kSumRow = GS_PAIR_GRAD_FLOATS + 1;
+#ifdef GS_FUSED_WPE
+#define GS_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(GS_FUSED_WPE, GS_FUSED_WPE)))
+#else
+#define GS_FUSED_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) GS_FUSED_ATTR void k_gather_project_bwd(gs_project_bwd_args a) {
+  __shared__ float s_sum[kBlock * kSumRow];
+  constexpr int LPG = 8, GPR = kBlock / LPG;  // lanes per Gaussian, Gaussians per round
+  const long long g0 = (long long)blockIdx.x * kBlock;
+#pragma unroll GS_FUSED_UNROLL
+  for (int r = 0; r < kBlock / GPR; ++r) {
+    const long long t = (g0 + r * GPR) * LPG + threadIdx.x;
+    float2 acc[kF2];
+    gather_slots<4, 2, 4>(a, 4u, t, acc);
+    if ((threadIdx.x % LPG) == 0) {
+      float *row = s_sum + (r * GPR + threadIdx.x / LPG) * kSumRow;
+#pragma unroll
+      for (int k = 0; k < kF2; ++k) {
+        row[2 * k] = acc[k].x;
+        row[2 * k + 1] = acc[k].y;
+      }
+    }
+  }
+  __syncthreads();
+  const long long g = g0 + threadIdx.x;
+  if (g >= a.g.n) return;
+  project_bwd_one<true>(a, (int)g, [&](float acc[GS_PAIR_GRAD_FLOATS]) {
+    const float *row = s_sum + threadIdx.x * kSumRow;
+#pragma unroll
+    for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = row[k];
+  });
+}
+
 // tile coordinates are packed in 12 bits (record word 11): images up to 65536 px a side
 
 // ======================================================== Adam ============
@@ -2569,11 +2106,10 @@ int cells_per_tile(int tile_size) {
   return qx * qx;
 }
 
-// gradient partials gs_blend_backward writes per list entry: the default
-// tile's waves combine kBwdCpw cells (k_blend_bwd_grp); other tiles one per cell
-int partial_groups(int tile_size) {
-  return tile_size == GS_DEFAULT_TILE ? 4 / kBwdCpw : cells_per_tile(tile_size);
-}
+// gradient partials gs_blend_backward writes per list entry: one per cell
+// (a wave combining a tile's cells wrote fewer and replayed slower:
+// tools/variants/README.md)
+int partial_groups(int tile_size) { return cells_per_tile(tile_size); }
 
 // tile_size in range, image non-empty, tile coordinates fit 12 bits
 bool cam_ok(const gs_camera &c) {
@@ -2768,8 +2304,9 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   if (!tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_forward");
   if (!a->ranges || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_acc || !a->pix_state ||
-      !a->live_bits || a->live_words <= 0)
+      !a->live_bits || a->live_words <= 0 || (a->num_pairs > 0 && !a->sorted_gauss))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_forward");
+  if (a->num_pairs < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative num_pairs", "gs_blend_forward");
   hipStream_t s = (hipStream_t)stream;
   const bool t16 = a->cam.tile_size == GS_DEFAULT_TILE;
   const long long cblocks = (long long)div_up((long long)a->tiles_x * a->tiles_y, 8) * 8LL * cells_per_tile(a->cam.tile_size);
@@ -2783,24 +2320,6 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   return check_launch("gs_blend_forward");
 }
 
-size_t gs_tile_order_size(int32_t num_tiles) { return num_tiles > 0 ? 4u * (size_t)((num_tiles + 7) & ~7) : 0; }
-
-gs_status gs_tile_order(const gs_order_args *a, gs_stream_t stream) {
-  if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_tile_order");
-  if (a->num_tiles < 0 || (a->cell_work && (a->cells < 1 || a->cells > 1024)))
-    return fail(GS_ERR_INVALID_ARG, "%s: bad num_tiles / cells", "gs_tile_order");
-  if (a->num_tiles == 0) return GS_OK;
-  if (!a->tile_order || !a->ranges) return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_order");
-  hipStream_t s = (hipStream_t)stream;
-  if (!a->cell_work)
-    k_tile_order<0><<<1, kOrdThreads, 0, s>>>(*a);
-  else if (a->cells == 4)
-    k_tile_order<1><<<1, kOrdThreads, 0, s>>>(*a);
-  else
-    k_tile_order<2><<<1, kOrdThreads, 0, s>>>(*a);
-  return check_launch("gs_tile_order");
-}
-
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_backward");
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_blend_backward");
@@ -2809,19 +2328,12 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!a->ranges || !a->sorted_gauss || !a->records || !a->pix_acc || !a->pix_state || !a->g_image ||
       !a->pair_grads || !a->slot_live || !a->live_bits || a->live_words <= 0)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_backward");
+  if (a->num_pairs < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative num_pairs", "gs_blend_backward");
   hipStream_t s = (hipStream_t)stream;
   const int num_tiles = a->tiles_x * a->tiles_y;
   if (num_tiles <= 0) return GS_OK;
   const long long blocks = (long long)div_up(num_tiles, 8) * 8LL * cells_per_tile(a->cam.tile_size);
   if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_backward");
-  if constexpr (kBwdCpw > 1) {  // variant builds only (measured slower)
-    if (a->cam.tile_size == GS_DEFAULT_TILE) {
-      // (8 XCD bands of ceil(tiles / 8) tiles, partial_groups waves per tile)
-      k_blend_bwd_grp<kBwdCpw><<<(unsigned)(div_up(num_tiles, 8) * 8LL * partial_groups(GS_DEFAULT_TILE)), kWave,
-                                 0, s>>>(*a);
-      return check_launch("gs_blend_backward");
-    }
-  }
   if (a->cam.tile_size == GS_DEFAULT_TILE)
     k_blend_bwd<true><<<(unsigned)blocks, kWave, 0, s>>>(*a);
   else
@@ -2843,6 +2355,11 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
                 "gs_project_backward");
   if (a->pair_grads && !cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
+  const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
+  if (hot && GS_FUSED_GATHER && partial_groups(a->cam.tile_size) == 4) {
+    k_gather_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
+    return check_launch("gs_project_backward");
+  }
   if (a->pair_grads) {
     const uint32_t ng = (uint32_t)partial_groups(a->cam.tile_size);
     if (ng == 1)
@@ -2854,7 +2371,6 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
     else
       k_gather_slots<4, 2><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
   }
-  const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
   if (hot)
     k_project_bwd<true><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   else
@@ -2885,18 +2401,5 @@ gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream) {
       c, make_int4(starts[0], starts[1], starts[2], starts[3]), make_int4(starts[4], starts[5], starts[6], starts[7]));
   return check_launch("gs_adam_step");
 }
-
-#ifdef GS_WAVE_TIMES
-// (variant builds only) which = 0: the last k_blend_fwd, 1: the last
-// k_blend_bwd; per workgroup (start, end, xcc << 32 | HW_ID), u64 each
-gs_status gs_debug_wave_times(int32_t which, void *host, size_t bytes) {
-  if (which < 0 || which > 1 || bytes > sizeof(g_wave_times[0]))
-    return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_debug_wave_times");
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_times), bytes, (size_t)which * sizeof(g_wave_times[0]),
-                          hipMemcpyDeviceToHost) != hipSuccess)
-    return fail(GS_ERR_LAUNCH, "%s: copy failed", "gs_debug_wave_times");
-  return GS_OK;
-}
-#endif
 
 }  // extern "C"

@@ -163,7 +163,7 @@ def _check_inputs(xyz: torch.Tensor):
 
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
-    __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_acc", "bwd_order",
+    __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_acc",
                  "pix_state", "live_bits", "big", "M", "T", "slot_live")
 
 
@@ -213,12 +213,6 @@ class _HostCounters:
         v = self.np[:4].tolist()
         return int(v[0]), int(v[1]), int(v[2]) & 0xFFFFFFFF, int(v[3]) & 0xFFFFFFFF
 _FUSE_FLAGS = os.environ.get("GS_FUSE_SLOT_FLAGS", "1") != "0"  # slot flags zeroed by gs_tile_ranges
-# blend launches dispatched heaviest tiles first (gs_tile_order): 1 both, "fwd" / "bwd" one, 0 none.
-# Off by default: at C3 the order saves 4-9 us per blend launch but its one-workgroup
-# sort costs ~14 us per launch (profiles/r03/experiments.md, "Dispatch order")
-_TILE_ORDER = os.environ.get("GS_TILE_ORDER", "0")
-_ORDER_FWD = _TILE_ORDER in ("1", "fwd")
-_ORDER_BWD = _TILE_ORDER in ("1", "bwd")
 # Depth-key windows (per process and device; these are guesses, a stale one
 # only costs a re-render, so host threads may race on them): the window
 # covers the union of the last _WINDOW_FRAMES frames' visible depth ranges, so
@@ -436,11 +430,6 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         depth = torch.empty((1, H, W), dtype=f32, device=dev)
         pix_acc = torch.empty((H * W, 4), dtype=f32, device=dev)
         pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
-        # dispatch orders of the blend launches (heaviest tiles first) and the
-        # forward's per-cell replay counts that order the backward
-        order_n = int(lib.gs_tile_order_size(num_tiles))
-        orders = torch.empty((2, order_n), dtype=i32, device=dev) if (_ORDER_FWD or _ORDER_BWD) else None
-        cell_work = torch.empty((num_tiles * cam.cells,), dtype=i32, device=dev) if need_grad and _ORDER_BWD else None
         # the T-sized buffers too, at a capacity guessed from the last frame on
         # this device, and the emission queued into them before the sync (it
         # drops entries past the capacity): its kernel time hides the
@@ -512,26 +501,12 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
                        L.big.data_ptr() + L.o_flags if need_grad else None, cam.groups)
     StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
-    fwd_order = None
-    if _ORDER_FWD:
-        StageTimer.mark("tile_order")
-        oa = N.GsOrderArgs(num_tiles, cam.cells, N.ptr(ranges), None, N.ptr(orders[0]))
-        N.check(lib.gs_tile_order(C.byref(oa), s), "gs_tile_order")
-        fwd_order = orders[0]
 
     fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), L.p_tv[alt.value], N.ptr(records),
                           N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state),
-                          L.p_live, L.live_words, N.ptr(pair_counts), N.ptr(fwd_order), N.ptr(cell_work))
+                          L.p_live, L.live_words, N.ptr(pair_counts), T)
     StageTimer.mark("blend_fwd")
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
-    fr.bwd_order = None
-    if cell_work is not None:
-        # the backward's order, from this frame's replay counts (queued now:
-        # one small launch between the two blends)
-        StageTimer.mark("tile_order")
-        oa = N.GsOrderArgs(num_tiles, cam.cells, N.ptr(ranges), N.ptr(cell_work), N.ptr(orders[1]))
-        N.check(lib.gs_tile_order(C.byref(oa), s), "gs_tile_order")
-        fr.bwd_order = orders[1]
     StageTimer.mark("~end_fwd")
     _T_SEEN[dev] = T  # (the next frame's guesses: after the launches)
     _record_depths(dev, zmin, zmax)
@@ -580,8 +555,7 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
-                              fr.live_bits.shape[1], N.ptr(pair_grads), N.ptr(slot_live),
-                              N.ptr(getattr(fr, "bwd_order", None)))
+                              fr.live_bits.shape[1], N.ptr(pair_grads), N.ptr(slot_live), fr.T)
         StageTimer.mark("blend_bwd")
         N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
     raw = cov3d is None

@@ -19,23 +19,17 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=7000)
-    ap.add_argument("--views", type=int, default=100)
-    ap.add_argument("--size", type=int, default=800)
-    ap.add_argument("--gt-gaussians", type=int, default=200_000)
-    ap.add_argument("--profile-iters", type=int, default=0,
-                    help="host profile (cProfile) of this many iterations after 100 warm ones, then exit")
-    a = ap.parse_args()
-    import __graft_entry__ as ge
-    pkg = ge.load_package()
+def build_scene(pkg, views=100, size=800, gt_gaussians=200_000, device=None):
+    """The C4 stand-in dataset: `views` cameras on a sphere of radius 4 around
+    a ball of `gt_gaussians` random Gaussians, each image rendered from them
+    at size x size (NeRF-synthetic layout, composited on black).  Returns the
+    loaded NeRFSyntheticDataset with 1/8 of the views held out as test views."""
     from test_training_cpu import look_at_c2w_gl, _png
-    dev = torch.device("cuda", 0)
+    dev = device if device is not None else torch.device("cuda", 0)
     tmp = tempfile.mkdtemp()
     os.makedirs(os.path.join(tmp, "train"))
     frames, rng = [], np.random.default_rng(0)
-    for i in range(a.views):
+    for i in range(views):
         th, ph = 2 * math.pi * rng.random(), math.asin(2 * rng.random() - 1) * 0.8
         C = 4.0 * np.array([math.cos(th) * math.cos(ph), math.sin(th) * math.cos(ph), math.sin(ph)])
         frames.append({"file_path": f"./train/r_{i}", "transform_matrix": look_at_c2w_gl(C).tolist()})
@@ -47,7 +41,7 @@ def main():
     ds = pkg.NeRFSyntheticDataset(tmp, device=dev)
     ds.load_cameras()
     g = torch.Generator().manual_seed(3)
-    n = a.gt_gaussians
+    n = gt_gaussians
     d = torch.randn(n, 3, generator=g)
     xyz = d / d.norm(dim=1, keepdim=True) * torch.rand(n, 1, generator=g) ** (1 / 3)
     gt = pkg.GaussianModel()
@@ -57,14 +51,36 @@ def main():
     r = pkg.GaussianRenderer()
     with torch.no_grad():
         for cam in ds.cameras:
-            cam._width = cam._height = a.size
+            cam._width = cam._height = size
             cam._FoVy = cam._FoVx
-            cam._image = r.render(cam, gt, pkg.RenderSettings(a.size, a.size, torch.zeros(3)))["image"].clone()
+            cam._image = r.render(cam, gt, pkg.RenderSettings(size, size, torch.zeros(3)))["image"].clone()
     ds.split_train_test(0.125)
-    cfg = pkg.TrainingConfig(iterations=a.iters, num_random_points=100_000, log_interval=500,
-                             densify_until_iter=min(15000, a.iters // 2), output_path=os.path.join(tmp, "out"))
+    ds.root = tmp
+    return ds
+
+
+def make_trainer(pkg, ds, iters=7000):
+    cfg = pkg.TrainingConfig(iterations=iters, num_random_points=100_000, log_interval=500,
+                             densify_until_iter=min(15000, iters // 2), output_path=os.path.join(ds.root, "out"))
     tr = pkg.GaussianTrainer(cfg, ds)
     tr.setup()
+    return tr
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=7000)
+    ap.add_argument("--views", type=int, default=100)
+    ap.add_argument("--size", type=int, default=800)
+    ap.add_argument("--gt-gaussians", type=int, default=200_000)
+    ap.add_argument("--profile-iters", type=int, default=0,
+                    help="host profile (cProfile) of this many iterations after 100 warm ones, then exit")
+    a = ap.parse_args()
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    ds = build_scene(pkg, a.views, a.size, a.gt_gaussians)
+    n = a.gt_gaussians
+    tr = make_trainer(pkg, ds, a.iters)
     if a.profile_iters:
         import cProfile
         import pstats
