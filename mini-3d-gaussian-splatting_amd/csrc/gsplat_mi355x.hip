@@ -1642,11 +1642,7 @@ __device__ __forceinline__ float lanes_sum(float v) {
   return v;
 }
 
-#ifndef GS_GATHER_HL1
-#define GS_GATHER_HL1 4
-#endif
-
-constexpr int kGatherHL1 = GS_GATHER_HL1;  // slot lanes per Gaussian with one partial group per slot
+constexpr int kGatherHL1 = 4;  // slot lanes per Gaussian with one partial group per slot
 
 constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
 
@@ -1971,53 +1967,6 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
         acc[2 * k + 1] = v.y;
       }
     }
-  });
-}
-
-// The training configuration at the default tile (four partial groups per
-// slot), gather and chain rule in one launch: the workgroup's 256 Gaussians'
-// partials are summed 32 Gaussians per round (8 lanes each, as
-// k_gather_slots<4, 2, 4>, the same fixed order: bit-identical sums) into
-// LDS, then thread t runs Gaussian t's chain rule from there -- the [n, 10]
-// sums never reach HBM (40 B written + 40 B read per Gaussian) and one launch
-// goes.  Rows padded to 11 floats (bank spread of the per-thread reads).
-#ifndef GS_FUSED_GATHER
-#define GS_FUSED_GATHER 1
-#endif
-#ifndef GS_FUSED_UNROLL
-#define GS_FUSED_UNROLL 1
-#endif
-constexpr int kSumRow = GS_PAIR_GRAD_FLOATS + 1;
-#ifdef GS_FUSED_WPE
-#define GS_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(GS_FUSED_WPE, GS_FUSED_WPE)))
-#else
-#define GS_FUSED_ATTR
-#endif
-__global__ __launch_bounds__(kBlock) GS_FUSED_ATTR void k_gather_project_bwd(gs_project_bwd_args a) {
-  __shared__ float s_sum[kBlock * kSumRow];
-  constexpr int LPG = 8, GPR = kBlock / LPG;  // lanes per Gaussian, Gaussians per round
-  const long long g0 = (long long)blockIdx.x * kBlock;
-#pragma unroll GS_FUSED_UNROLL
-  for (int r = 0; r < kBlock / GPR; ++r) {
-    const long long t = (g0 + r * GPR) * LPG + threadIdx.x;
-    float2 acc[kF2];
-    gather_slots<4, 2, 4>(a, 4u, t, acc);
-    if ((threadIdx.x % LPG) == 0) {
-      float *row = s_sum + (r * GPR + threadIdx.x / LPG) * kSumRow;
-#pragma unroll
-      for (int k = 0; k < kF2; ++k) {
-        row[2 * k] = acc[k].x;
-        row[2 * k + 1] = acc[k].y;
-      }
-    }
-  }
-  __syncthreads();
-  const long long g = g0 + threadIdx.x;
-  if (g >= a.g.n) return;
-  project_bwd_one<true>(a, (int)g, [&](float acc[GS_PAIR_GRAD_FLOATS]) {
-    const float *row = s_sum + threadIdx.x * kSumRow;
-#pragma unroll
-    for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = row[k];
   });
 }
 
@@ -2356,10 +2305,6 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   if (a->pair_grads && !cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
   const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
-  if (hot && GS_FUSED_GATHER && partial_groups(a->cam.tile_size) == 4) {
-    k_gather_project_bwd<<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
-    return check_launch("gs_project_backward");
-  }
   if (a->pair_grads) {
     const uint32_t ng = (uint32_t)partial_groups(a->cam.tile_size);
     if (ng == 1)
