@@ -441,6 +441,7 @@ def cpu_baseline(scene, W, H, cot, threads):
         r = orc.render_backward(s, gi, ga, gd, nthreads=c)
         dt = time.perf_counter() - t0
         sweep[str(c)] = round(H * W / dt / 1e6, 4)
+        print(f"cpu baseline: {c} threads {dt:.2f} s", file=sys.stderr, flush=True)  # (progress)
         if ref is None:
             ref = r
         if best is None or dt < best[1]:

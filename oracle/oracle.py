@@ -31,7 +31,7 @@ class _Scene(C.Structure):
         ("fovx", C.c_double), ("fovy", C.c_double),
         ("wv", _fp), ("radius_min", C.c_float), ("radius_max", C.c_float),
         ("bg", _fp), ("xyz", _fp), ("cov3d", _fp), ("color_logits", _fp),
-        ("opacity", _fp),
+        ("opacity", _fp), ("force_neval", C.POINTER(C.c_int32)),
     ]
 
 
@@ -103,6 +103,10 @@ class Scene:
     tile: int = 16
     radius_min: float = 0.01
     radius_max: float = 50.0
+    # [H,W] int32 or None: decision-forced replay -- pixel p evaluates exactly
+    # its first force_neval[p] list entries, with no termination test of its
+    # own (another renderer's per-pixel n_eval; gs_oracle.c gso_scene)
+    force_neval: Optional[np.ndarray] = None
 
 
 def _scene_struct(s: Scene, keep: list) -> _Scene:
@@ -111,13 +115,18 @@ def _scene_struct(s: Scene, keep: list) -> _Scene:
         cov3d=_f32(s.cov3d).reshape(-1, 9), color_logits=_f32(s.color_logits).reshape(-1, 3),
         opacity=_f32(s.opacity).reshape(-1),
     )
+    fn = None
+    if s.force_neval is not None:
+        fn = np.ascontiguousarray(np.asarray(s.force_neval, dtype=np.int32).reshape(int(s.height), int(s.width)))
+        arrs["force_neval"] = fn
     keep.append(arrs)
     n = arrs["xyz"].shape[0]
     cw = int(s.width if s.cam_width is None else s.cam_width)
     ch = int(s.height if s.cam_height is None else s.cam_height)
     return _Scene(n, int(s.width), int(s.height), int(s.tile), cw, ch, float(s.fovx), float(s.fovy),
                   _p(arrs["wv"]), float(s.radius_min), float(s.radius_max), _p(arrs["bg"]),
-                  _p(arrs["xyz"]), _p(arrs["cov3d"]), _p(arrs["color_logits"]), _p(arrs["opacity"]))
+                  _p(arrs["xyz"]), _p(arrs["cov3d"]), _p(arrs["color_logits"]), _p(arrs["opacity"]),
+                  C.cast(None, C.POINTER(C.c_int32)) if fn is None else fn.ctypes.data_as(C.POINTER(C.c_int32)))
 
 
 def _alloc_fwd(n: int, h: int, w: int, margins: bool = False):

@@ -566,6 +566,34 @@ def _scene_vs_oracle(pkg, cuda, sc, W, H, bg, seed=1, renderer_kw=None, knife=Tr
             msg += f"; {G.grad_rel_err(d, r, touch):.3g} over the {int(touch.sum())} touching them"
         print(msg)
         errs += G.check_grad(name, d, r, rows=rows)
+    if touch.any():
+        # Round-3 review (weak 8): the exempted Gaussians checked too.  The
+        # oracle replays the frame again with the GPU's per-pixel termination
+        # points (decision-forced: gso_scene.force_neval = the forward's n_eval,
+        # every skip decision still its own), so a pixel whose A lands within
+        # an ulp of 0.995 on one side and not the other is compared on the same
+        # chain: image and EVERY Gaussian's gradient at the standard tolerances.
+        RZ = pkg.rasterizer
+        camp = pkg.camera_params(Cam(W, H, sc.fovx, sc.fovy, wv=wv), pkg.RenderSettings(H, W, torch.tensor(bg)),
+                                 **{k: kw[k] for k in ("radius_min", "radius_max", "tile_size") if k in kw})
+        with torch.no_grad():
+            fr = RZ.forward_pipeline(camp, m._xyz, None, m._scaling, m._rotation, m._features_dc[:, 0, :],
+                                     torch.sigmoid(m._opacity).squeeze(1))[-1]
+        neval = fr.pix_state[:, 1].contiguous().view(torch.int32).view(H, W).cpu().numpy()
+        osc.force_neval = neval
+        reff = G.oracle().render_backward(osc, gi, ga, gd, nthreads=min(16, os.cpu_count() or 1))
+        badf = G.pixel_errors(o, reff)
+        print(f"{label} decision-forced oracle: {int(badf.sum())} of {H * W} px out of tolerance")
+        errs += G.check_image(o, reff)
+        dsf, drf = G.oracle().covariance_backward(sc.scaling.numpy(), sc.rotation.numpy(), reff["grads"]["cov3d"])
+        forced = (("xyz", _np(m._xyz.grad), reff["grads"]["xyz"]), ("scaling", _np(m._scaling.grad), dsf),
+                  ("rotation", _np(m._rotation.grad), drf),
+                  ("features_dc", _np(m._features_dc.grad)[:, 0], reff["grads"]["color_logits"]),
+                  ("opacity", _np(m._opacity.grad)[:, 0], reff["grads"]["opacity"] * op * (1 - op)))
+        for name, d, r in forced:
+            print(f"{label} decision-forced grad {name}: max err / max|ref| = {G.grad_rel_err(d, r):.3g} over all "
+                  f"{d.shape[0]} Gaussians ({G.grad_rel_err(d, r, touch):.3g} over the {int(touch.sum())} formerly exempt)")
+            errs += [f"forced: {e}" for e in G.check_grad(name, d, r)]
     return errs, bad, edge
 
 
