@@ -12,6 +12,8 @@ timeout -k 10 120 ./build/sortbench > "$O/sortbench.log" 2>&1 || { echo "sortben
 cat "$O/sortbench.log"
 timeout -k 10 300 python -u -m pytest tests/test_c4_training_gpu.py -x -q -s --timeout 240 --timeout-method thread > "$O/c4.log" 2>&1 || { echo "c4 failed"; tail -20 "$O/c4.log"; exit 1; }
 grep '"workload"' "$O/c4.log"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -s --timeout 240 --timeout-method thread -k "c3_full or c2_full" > "$O/c3c2.log" 2>&1 || { echo "c3/c2 failed"; grep -E "decision-forced|px out|FAIL|Error" "$O/c3c2.log" | head -40; exit 1; }
+grep -E "decision-forced|out of tolerance|grad " "$O/c3c2.log"
 GS_ALLREDUCE_CHUNKS=4 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
   --master-addr 127.0.0.1 --master-port 29551 bench.py --gpus 1 --steps 20 --warmup 3 --force-dist \
   --no-cpu-baseline > "$O/rccl_world1.log" 2>&1 || { echo "rccl world1 failed"; tail -20 "$O/rccl_world1.log"; exit 1; }
