@@ -304,7 +304,8 @@ def main():
             "warmup": a.warmup, "spinup_steps": a.spinup_steps, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C3: 1M synthetic Gaussians (SURVEY 8d), 1920x1080, 16x16 tiles, "
-                                   "render fwd+bwd" + ("" if opt is None else " + grad all-reduce + Adam step"),
+                                   "render fwd+bwd" + (" + grad all-reduce" if reducer is not None else "")
+                                   + ("" if opt is None else " + Adam step"),
                        "gaussians": n, "width": W, "height": H, "views_per_step": world,
                        "parallelism": f"dp{world} (one view per GPU)", "visible": M, "tile_touches": T,
                        "records_consumed": R, "evaluated_pairs": E, "contributing_pairs": Cc},

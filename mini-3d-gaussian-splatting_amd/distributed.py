@@ -165,9 +165,16 @@ class GradAllReduce:
         self._native = None
         self.native_status = {"native": False, "rccl_nranks": None, "self_check_err": None,
                               "fallback_reason": "GS_DP_NATIVE=0" if self._avg else "backend is not nccl"}
-        if self._avg and os.environ.get("GS_DP_NATIVE", "1") != "0":
+        mode = os.environ.get("GS_DP_NATIVE", "1")
+        # "force": try native RCCL over any backend's process group (a rehearsal
+        # of the establishment protocol, e.g. two gloo ranks on one GPU, where
+        # RCCL refuses the duplicate device and every rank must fall back)
+        if (self._avg and mode != "0") or (mode == "force" and torch.cuda.is_available()
+                                            and hasattr(dist, "is_initialized") and dist.is_initialized()):
             self._native = _native_comm(dist, group)
             self.native_status = dict(native_status())
+            if self._native is not None:
+                self._avg = True  # ncclAvg forms the mean (no division after the reduction)
 
     def _bucket(self) -> torch.Tensor:
         sizes = [p.numel() for p in self.params]

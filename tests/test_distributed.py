@@ -53,26 +53,30 @@ def _from_value(ts):
     return [None if a is None else torch.from_numpy(a) for a in ts]
 
 
-def test_grad_all_reduce_mean_gloo():
+@pytest.mark.parametrize("world", [2, 3])
+def test_grad_all_reduce_mean_gloo(world):
+    """The mean over the ranks (world 3: a mean that is not a power-of-two
+    scaling); a rank with no grad for a parameter counts as zeros."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict()
-    for _ in range(2):
+    for _ in range(world):
         r, local, reduced = q.get(timeout=120)
         res[r] = (_from_value(local), _from_value(reduced))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     for i in range(5):
-        a = res[0][0][i]
-        b = res[1][0][i] if res[1][0][i] is not None else torch.zeros_like(a)
-        exp = (a + b) / 2
-        assert torch.allclose(res[0][1][i], exp, atol=1e-6)
-        assert torch.equal(res[0][1][i], res[1][1][i])  # replicas stay identical
+        loc = [res[r][0][i] for r in range(world)]
+        ref = next(t for t in loc if t is not None)
+        exp = sum((t if t is not None else torch.zeros_like(ref)).double() for t in loc) / world
+        assert torch.allclose(res[0][1][i].double(), exp, atol=1e-6)
+        for r in range(1, world):
+            assert torch.equal(res[0][1][i], res[r][1][i])  # replicas stay identical
 
 
 def _worker_zero_copy(rank, world, port, q, ranges=None):
