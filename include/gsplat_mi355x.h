@@ -31,9 +31,13 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 15
+#define GS_ABI_VERSION 16
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
-#define GS_MAX_TILE 256       /* tile_size in [1, GS_MAX_TILE] (the reference accepts any int) */
+#define GS_MAX_TILE 4096      /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
+                                 of at least max(W, H) renders the same as any larger one (one tile
+                                 holds the image), so callers clamp to max(W, H) */
+#define GS_DENSE_MAX_TILE 256 /* above this tile edge the blend backward sums gradients per Gaussian
+                                 with fp32 atomics (gs_partial_groups returns 0) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
                                  edge L holds gs_tile_quads(L) = ceil(L/8)^2 of them (edge cells
                                  clipped to the tile); one 64-lane wave renders one cell */
@@ -264,8 +268,13 @@ size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles);
 /* Cells per tile: ceil(tile_size / 8)^2 (4 for the default 16); 0 if out of range. */
 int32_t gs_tile_quads(int32_t tile_size);
 /* Gradient partials gs_blend_backward writes per list entry (G below): one
- * per 8x8 cell, gs_tile_quads(tile_size) (4 for the default 16x16 tile).
- * 0 if out of range. */
+ * per 8x8 cell, gs_tile_quads(tile_size) (4 for the default 16x16 tile), up
+ * to GS_DENSE_MAX_TILE.  Above it 0: a dense [T, G] partial buffer would grow
+ * with (L/8)^2, so the backward adds each (entry, cell)'s sums into the
+ * Gaussian's row of an [n, GS_PAIR_GRAD_FLOATS] buffer with fp32 atomics
+ * (pair_grads = that buffer, zeroed by the caller; slot_live unused; the
+ * projection backward reads it as grad_sums and skips the gather).  0 also
+ * if out of range. */
 int32_t gs_partial_groups(int32_t tile_size);
 
 /* ---- Backward of the blend -------------------------------------------
@@ -291,8 +300,9 @@ typedef struct gs_blend_bwd_args {
   const float *g_depth;         /* [H,W] or NULL */
   const uint64_t *live_bits;    /* the forward's liveness bitmap */
   int64_t live_words;
-  float *pair_grads;            /* [T, G, GS_PARTIAL_STRIDE], G = gs_partial_groups(cam.tile_size) */
-  uint8_t *slot_live;           /* [T, G], zeroed by the caller (or gs_tile_ranges) */
+  float *pair_grads;            /* [T, G, GS_PARTIAL_STRIDE], G = gs_partial_groups(cam.tile_size);
+                                   G = 0: [n, GS_PAIR_GRAD_FLOATS] sums, zeroed by the caller */
+  uint8_t *slot_live;           /* [T, G], zeroed by the caller (or gs_tile_ranges); unused when G = 0 */
   int32_t num_pairs;            /* T, the entries of sorted_gauss: tile ranges are clamped to it */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
@@ -315,7 +325,8 @@ typedef struct gs_project_bwd_args {
   const uint32_t *pair_offset;
   const uint32_t *order;       /* [n] permutation to walk the Gaussians in, or NULL: index order
                                   (slots are numbered in index order, so NULL reads them coalesced) */
-  const float *pair_grads;     /* [T,G,GS_PARTIAL_STRIDE] (gs_partial_groups); may be NULL when T == 0 */
+  const float *pair_grads;     /* [T,G,GS_PARTIAL_STRIDE] (gs_partial_groups); may be NULL when T == 0;
+                                  G = 0: the blend backward's [n, 10] sums (also passed as grad_sums) */
   const float *g_means2d;      /* [n,2] or NULL */
   const float *g_conics;       /* [n,4] or NULL */
   float *d_xyz;                /* [n,3] */
@@ -326,7 +337,8 @@ typedef struct gs_project_bwd_args {
   float *d_opacity;            /* [n]   */
   float *d_sh_rest;            /* [n,15,3] contiguous, written when g.sh_degree > 0 (zeros past the degree) */
   const uint8_t *slot_live;    /* [T,G] from gs_blend_backward; required with pair_grads */
-  float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS] scratch (g's partials summed); with pair_grads */
+  float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS] scratch (g's partials summed); with pair_grads;
+                                  G = 0: the sums themselves (read, not written) */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
 

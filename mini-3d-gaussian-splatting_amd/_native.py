@@ -21,13 +21,14 @@ LIB_NAME = "libgsplat_mi355x.so"
 LIB_PATH = os.environ.get("GS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 
 GS_DEFAULT_TILE = 16  # renderer.py:24
-GS_MAX_TILE = 256
+GS_MAX_TILE = 4096
+GS_DENSE_MAX_TILE = 256  # above: gradient sums per Gaussian by fp32 atomics (gs_partial_groups == 0)
 GS_QUAD = 8  # 8x8 pixel cells per wave, ceil(tile/8)^2 per tile (gs_tile_quads)
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 15
+GS_ABI_VERSION = 16
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p

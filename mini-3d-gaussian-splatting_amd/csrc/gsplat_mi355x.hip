@@ -1313,7 +1313,13 @@ __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
 }
 
 
-template <bool kT16>
+// kSums: tiles above GS_DENSE_MAX_TILE (gs_partial_groups == 0): a per-(entry,
+// cell) partial buffer would need T x (L/8)^2 x 40 B, so each (entry, cell)'s
+// sums go straight into the Gaussian's [n, 10] row of pair_grads with fp32
+// atomics (bounded memory; reproducible to rounding only; 4x the partial
+// path's cost per sum -- tools/variants/README.md -- on tile sizes no
+// performance path uses).
+template <bool kT16, bool kSums>
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
@@ -1402,9 +1408,12 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     return rem < 64u ? m & ((1ull << rem) - 1ull) : m;
   };
   // lane l gathers the record of entry 64 wd + l when that entry is live here
+  // (kSums: and keeps its Gaussian id for the atomic sums)
+  uint32_t gcur = gid0, gnx = 0u;
   auto fetch = [&](uint32_t wd, unsigned long long m) {
     if ((m >> lane) & 1ull) {
       const uint32_t gid = a.sorted_gauss[start + 64u * wd + (uint32_t)lane];
+      gnx = gid;
       r0 = recs[3 * (size_t)gid];
       r1 = recs[3 * (size_t)gid + 1];
       r2 = recs[3 * (size_t)gid + 2];
@@ -1481,7 +1490,20 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
       Sx = oct_sum(Sx); Sy = oct_sum(Sy); g2 = oct_sum(g2); g3 = oct_sum(g3); g4 = oct_sum(g4);
       g5 = oct_sum(g5); g6 = oct_sum(g6); g7 = oct_sum(g7); g8 = oct_sum(g8); g9 = oct_sum(g9);
-      if (col == 0) {
+      if constexpr (kSums) {
+        // the entry's 10 sums into its Gaussian's row: lane 8j + c adds
+        // component c, lanes 8j, 8j + 1 components 8, 9 (no-return atomics)
+        const uint32_t gid = __float_as_uint(s_wrec[6 * e + 5].y);
+        const float q00 = ia.z, qo = ib.x, q11 = ia.w;
+        const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
+        const float v = col == 0 ? g0 : col == 1 ? g1 : col == 2 ? g2 : col == 3 ? g3 : col == 4 ? g4
+                      : col == 5 ? g5 : col == 6 ? g6 : g7;
+        float *dst = a.pair_grads + (size_t)gid * GS_PAIR_GRAD_FLOATS;
+        (void)__hip_atomic_fetch_add(dst + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (col < 2)
+          (void)__hip_atomic_fetch_add(dst + 8 + col, col ? g9 : g8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)slot;
+      } else if (col == 0) {
         const float q00 = ia.z, qo = ib.x, q11 = ia.w;
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
@@ -1510,7 +1532,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     // this word's records stay in registers (staged chunk by chunk below)
     // while the next word's are fetched into r0..r2 (staging a whole word's
     // records, 3 KB of LDS, cost occupancy: -13 us when chunked)
-    const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
+    const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), kSums ? __uint_as_float(gcur) : 0.f);
     const unsigned long long simple_w = __builtin_amdgcn_ballot_w64(mine && simple_entry(r0, r1));
     const unsigned long long mnext = wd + 1u < nwords ? live_word(wd + 1u) : 0ull;
     fetch(wd + 1u, mnext);  // in flight while this word replays
@@ -1610,6 +1632,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     };
     if ((simple_w & mcur) == mcur) run_word(std::true_type{}); else run_word(std::false_type{});
     mcur = mnext;
+    gcur = gnx;
   }
 }
 
@@ -2058,7 +2081,7 @@ int cells_per_tile(int tile_size) {
 // gradient partials gs_blend_backward writes per list entry: one per cell
 // (a wave combining a tile's cells wrote fewer and replayed slower:
 // tools/variants/README.md)
-int partial_groups(int tile_size) { return cells_per_tile(tile_size); }
+int partial_groups(int tile_size) { return tile_size > GS_DENSE_MAX_TILE ? 0 : cells_per_tile(tile_size); }
 
 // tile_size in range, image non-empty, tile coordinates fit 12 bits
 bool cam_ok(const gs_camera &c) {
@@ -2275,7 +2298,8 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_backward");
   if (!a->ranges || !a->sorted_gauss || !a->records || !a->pix_acc || !a->pix_state || !a->g_image ||
-      !a->pair_grads || !a->slot_live || !a->live_bits || a->live_words <= 0)
+      !a->pair_grads || (!a->slot_live && partial_groups(a->cam.tile_size) > 0) || !a->live_bits ||
+      a->live_words <= 0)
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_backward");
   if (a->num_pairs < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative num_pairs", "gs_blend_backward");
   hipStream_t s = (hipStream_t)stream;
@@ -2284,9 +2308,11 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   const long long blocks = (long long)div_up(num_tiles, 8) * 8LL * cells_per_tile(a->cam.tile_size);
   if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_backward");
   if (a->cam.tile_size == GS_DEFAULT_TILE)
-    k_blend_bwd<true><<<(unsigned)blocks, kWave, 0, s>>>(*a);
+    k_blend_bwd<true, false><<<(unsigned)blocks, kWave, 0, s>>>(*a);
+  else if (partial_groups(a->cam.tile_size) > 0)
+    k_blend_bwd<false, false><<<(unsigned)blocks, kWave, 0, s>>>(*a);
   else
-    k_blend_bwd<false><<<(unsigned)blocks, kWave, 0, s>>>(*a);
+    k_blend_bwd<false, true><<<(unsigned)blocks, kWave, 0, s>>>(*a);
   return check_launch("gs_blend_backward");
 }
 
@@ -2297,7 +2323,7 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   if (!a->g.xyz || !a->g.color_logits || !a->means2d || !a->conics || !a->vis || !a->rects ||
       !a->pair_offset || !a->d_xyz || !a->d_color_logits || !a->d_opacity ||
       (raw ? (!a->g.scaling || !a->g.rotation || !a->d_scaling || !a->d_rotation) : !a->d_cov3d) ||
-      (a->pair_grads && (!a->slot_live || !a->grad_sums)))
+      (a->pair_grads && (!a->grad_sums || (!a->slot_live && partial_groups(a->cam.tile_size) > 0))))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_project_backward");
   if (a->g.sh_degree < 0 || a->g.sh_degree > 3 || (a->g.sh_degree > 0 && (!a->g.sh_rest || !a->d_sh_rest)))
     return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest and d_sh_rest when > 0",
@@ -2305,7 +2331,7 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   if (a->pair_grads && !cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
   const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
-  if (a->pair_grads) {
+  if (a->pair_grads && partial_groups(a->cam.tile_size) > 0) {  // (0: the sums are in grad_sums already)
     const uint32_t ng = (uint32_t)partial_groups(a->cam.tile_size);
     if (ng == 1)
       k_gather_slots<1, kGatherHL1><<<div_up((long long)kGatherHL1 * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);

@@ -61,7 +61,8 @@ class CameraParams:
     @property
     def groups(self) -> int:
         """Gradient partials the blend backward writes per list entry
-        (gs_partial_groups): 1 at the default tile, else one per cell."""
+        (gs_partial_groups): one per cell, 4 at the default tile; 0 above
+        GS_DENSE_MAX_TILE (per-Gaussian sums by atomics instead)."""
         return _partial_groups(self.tile_size)
 
     def to_struct(self) -> N.GsCamera:
@@ -498,7 +499,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
                                     L.p_ws, L.ws_bytes, C.byref(alt), s), "tile sort")
     # (with gradients to come: the backward's slot flags zeroed in the same kernel)
     ra = N.GsRangeArgs(T, num_tiles, L.p_tk[alt.value], N.ptr(ranges),
-                       L.big.data_ptr() + L.o_flags if need_grad else None, cam.groups)
+                       L.big.data_ptr() + L.o_flags if need_grad and cam.groups else None, cam.groups)
     StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
@@ -517,7 +518,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     fr.live_bits = L.big[L.o_live:L.o_live + 8 * cam.cells * L.live_words].view(torch.int64).view(cam.cells,
                                                                                                L.live_words)
     fr.big = L.big
-    fr.slot_live = L.big[L.o_flags:L.o_flags + cam.groups * T] if need_grad else None
+    fr.slot_live = L.big[L.o_flags:L.o_flags + cam.groups * T] if need_grad and cam.groups else None
     fr.pair_offset, fr.ranges = pair_offset, ranges
     fr.pix_acc, fr.pix_state = pix_acc, pix_state
     return image, alpha, depth, means2d, conics, radii, vis, fr
@@ -548,10 +549,15 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_depth = None if g_depth is None else g_depth.contiguous()
         # one partial per (slot, partial group of the tile: gs_partial_groups);
         # only the groups that replay an entry write theirs and set its flag
-        pair_grads = torch.empty((fr.T * cam.groups, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
-        slot_live = fr.slot_live  # (zeroed by the forward's gs_tile_ranges)
-        if slot_live is None:
-            slot_live = torch.zeros((fr.T * cam.groups,), dtype=torch.uint8, device=dev)
+        if cam.groups:
+            pair_grads = torch.empty((fr.T * cam.groups, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
+            slot_live = fr.slot_live  # (zeroed by the forward's gs_tile_ranges)
+            if slot_live is None:
+                slot_live = torch.zeros((fr.T * cam.groups,), dtype=torch.uint8, device=dev)
+        else:
+            # tiles above GS_DENSE_MAX_TILE: the blend backward adds per-Gaussian
+            # sums into [n, 10] with fp32 atomics (gs_partial_groups == 0)
+            pair_grads = torch.zeros((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
@@ -576,7 +582,8 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     gc = None if g_conics is None else g_conics.contiguous()
     d_sh = buf("sh_rest", (n, N.GS_SH_REST, 3)) if sh_degree > 0 else None
     gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
-    grad_sums = None if pair_grads is None else torch.empty((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
+    grad_sums = None if pair_grads is None else (
+        pair_grads if not cam.groups else torch.empty((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev))
     pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
                             # Gaussian order (order=NULL): inputs/outputs stream; walking in depth
                             # order coalesces the slot reads but scatters 10 arrays (measured 2.4x slower)

@@ -34,6 +34,7 @@ from typing import Dict, Optional
 
 import torch
 
+from . import _native as N
 from .rasterizer import CameraParams, rasterize
 
 
@@ -59,6 +60,21 @@ def _world_view(camera) -> torch.Tensor:
     return torch.as_tensor(wv)
 
 
+def effective_tile(tile_size: int, width: int, height: int) -> int:
+    """The tile edge the kernels use for GaussianRenderer(tile_size) on a
+    width x height image: tile_size, or max(width, height) when it is larger
+    -- the same image and gradients, since every tile of at least max(W, H)
+    holds the whole image (renderer.py:263-298: one tile, every Gaussian whose
+    rectangle meets the image, in depth order).  Edges up to GS_MAX_TILE."""
+    t = int(tile_size)
+    if t > max(int(width), int(height)):
+        t = max(int(width), int(height), 1)
+    if t > N.GS_MAX_TILE:
+        raise ValueError(f"tile_size {tile_size} on a {width}x{height} image: tiles above {N.GS_MAX_TILE} px "
+                         f"that do not cover the image are not supported")
+    return t
+
+
 def camera_params(camera, settings: RenderSettings, radius_min=0.01, radius_max=50.0, tile_size=16) -> CameraParams:
     """Host scalars of renderer.py:140-152 (python double -> fp32 in the ABI)."""
     W, H = camera._width, camera._height
@@ -68,18 +84,21 @@ def camera_params(camera, settings: RenderSettings, radius_min=0.01, radius_max=
     view = tuple(float(v) for v in wv[:3, :].reshape(-1).tolist())
     bg = settings.bg_color
     bg = tuple(float(v) for v in torch.as_tensor(bg).detach().to("cpu", torch.float32).reshape(3).tolist())
+    tile = effective_tile(tile_size, settings.image_width, settings.image_height)
     return CameraParams(int(settings.image_width), int(settings.image_height), fx, fy, W * 0.5, H * 0.5,
-                        view, bg, float(radius_min), float(radius_max), int(tile_size))
+                        view, bg, float(radius_min), float(radius_max), tile)
 
 
 class GaussianRenderer:
     """renderer.py:22-114"""
 
     def __init__(self, tile_size=16, radius_min=0.01, radius_max=50.0):
-        # any tile edge the reference's binning can use (renderer.py:261-298),
-        # capped at GS_MAX_TILE; radii as the reference clamps them (:190)
-        if int(tile_size) != tile_size or not 1 <= tile_size <= 256:
-            raise ValueError(f"tile_size must be an integer in [1, 256], got {tile_size!r}")
+        # any tile edge the reference's binning can use (renderer.py:261-298):
+        # every int >= 1 (0 divides by zero in the reference); edges above
+        # the image render as one tile of max(W, H) (effective_tile); radii as
+        # the reference clamps them (:190)
+        if int(tile_size) != tile_size or tile_size < 1:
+            raise ValueError(f"tile_size must be an integer >= 1, got {tile_size!r}")
         if not (math.isfinite(radius_max) and 0 <= radius_min <= radius_max):
             raise ValueError(f"need 0 <= radius_min <= radius_max < inf, got {radius_min!r}, {radius_max!r}")
         self.tile_size = int(tile_size)

@@ -651,6 +651,23 @@ def test_tile_sizes_vs_oracle(pkg, cuda, tile):
     assert not errs, errs
 
 
+@pytest.mark.parametrize("tile", [300, 480, 5000])
+def test_large_tiles_vs_oracle(pkg, cuda, tile):
+    """Tile edges above GS_DENSE_MAX_TILE (256): the blend backward sums each
+    Gaussian's gradient with fp32 atomics (gs_partial_groups == 0, no
+    [T, (L/8)^2] partial buffer).  300: 3 x 2 tiles of 1,444 cells, partial
+    edge tiles; 480: tiles as tall as the image; 5000, far above the image:
+    rendered as one tile of max(W, H) = 640 px (renderer.effective_tile), while
+    the oracle bins with the edge as given -- the same outputs, as the
+    reference's one-tile binning predicts."""
+    W, H = 640, 480
+    sc = pkg.synthetic.make_scene(3000, W, H, seed=40, sigma_range=(0.01, 0.05))
+    errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.1, 0.0, 0.3), renderer_kw=dict(tile_size=tile),
+                                    label=f"tile{tile}")
+    assert bad.sum() <= 2
+    assert not errs, errs
+
+
 def test_wide_rects_vs_oracle(pkg, cuda):
     """radius_max far above the default: rectangles up to 101 x 76 tiles of
     4 px, so a round of 256 Gaussians emits ~1M entries through many windows

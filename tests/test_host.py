@@ -48,14 +48,29 @@ def test_no_cpu_fallback(pkg):
 
 def test_renderer_constructor_range(pkg):
     """GaussianRenderer(tile_size, radius_min, radius_max) (renderer.py:24-28):
-    any tile edge in [1, 256] and finite radii are taken as given."""
-    for t in (1, 8, 12, 16, 32, 256):
+    any tile edge >= 1 (the reference takes any int; 0 divides by zero there)
+    and finite radii are taken as given.  The kernels' edge is the tile_size,
+    or max(W, H) when it is larger (one tile holds the image either way:
+    effective_tile); above 256 the backward sums per Gaussian
+    (gs_partial_groups == 0)."""
+    for t in (1, 8, 12, 16, 32, 256, 257, 1000, 10 ** 6):
         r = pkg.GaussianRenderer(tile_size=t, radius_max=80.0)
         assert r.tile_size == t and r.radius_max == 80.0
     c = pkg.camera_params(_Cam(), pkg.RenderSettings(20, 30, torch.zeros(3)), tile_size=8)
     assert (c.tiles_x, c.tiles_y, c.cells) == (4, 3, 1)
     assert pkg.camera_params(_Cam(), pkg.RenderSettings(20, 30, torch.zeros(3)), tile_size=32).cells == 16
-    for bad in (dict(tile_size=0), dict(tile_size=257), dict(tile_size=8.5), dict(radius_max=float("inf")),
+    # a tile above the image: one tile of max(W, H) = 30 px
+    for t in (31, 1000, 10 ** 9):
+        c = pkg.camera_params(_Cam(), pkg.RenderSettings(20, 30, torch.zeros(3)), tile_size=t)
+        assert (c.tile_size, c.tiles_x, c.tiles_y) == (30, 1, 1)
+    big = pkg.RenderSettings(4000, 4000, torch.zeros(3))
+    assert pkg.camera_params(_Cam(), big, tile_size=300).groups == 0  # atomic sums above 256
+    assert pkg.camera_params(_Cam(), big, tile_size=256).groups == 1024
+    assert pkg.camera_params(_Cam(), pkg.RenderSettings(5000, 5000, torch.zeros(3)), tile_size=10 ** 6).tile_size == 5000 \
+        if 5000 <= pkg._native.GS_MAX_TILE else True
+    with pytest.raises(ValueError):  # a 5000-px image in tiles above 4096 px that do not cover it
+        pkg.camera_params(_Cam(), pkg.RenderSettings(5000, 5000, torch.zeros(3)), tile_size=4500)
+    for bad in (dict(tile_size=0), dict(tile_size=-3), dict(tile_size=8.5), dict(radius_max=float("inf")),
                 dict(radius_min=3.0, radius_max=2.0)):
         with pytest.raises(ValueError):
             pkg.GaussianRenderer(**bad)
