@@ -159,6 +159,14 @@ class GaussianRenderer:
         image, alpha, depth, means2d, conics, radii, vis = rasterize(
             cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=fused,
             sh_rest=sh_rest, sh_degree=sh_degree, grad_dest=grad_dest)
+        # the reference's output dtypes (renderer.py:74-83, :273-275, :359-367):
+        # the projection outputs in the Gaussians' dtype, image in the
+        # background's (out_rgb starts as bg), alpha / depth float32 (zeros of
+        # the default dtype).  Computed in fp32 here either way.
+        if xyz.dtype == torch.float64:
+            means2d, conics, radii = means2d.double(), conics.double(), radii.double()
+        if torch.as_tensor(settings.bg_color).dtype == torch.float64:
+            image = image.double()
         return {
             "image": image,
             "alpha": alpha,

@@ -916,6 +916,13 @@ def test_float64_inputs_cast(pkg, cuda):
     b = pkg.GaussianRenderer().render(cam, g64, st)
     for k in ("image", "alpha", "depth"):
         assert torch.equal(a[k], b[k]), k
+    # the reference's output dtypes: projection outputs in the input dtype,
+    # image in the background's, alpha / depth float32
+    for k in ("viewspace_points", "conics", "radii"):
+        assert b[k].dtype == torch.float64 and torch.equal(b[k].float(), a[k]), k
+    assert b["image"].dtype == torch.float32 and b["alpha"].dtype == b["depth"].dtype == torch.float32
+    st64 = pkg.RenderSettings(64, 64, torch.zeros(3, dtype=torch.float64))
+    assert pkg.GaussianRenderer().render(cam, g64, st64)["image"].dtype == torch.float64
     (a["image"].sum() + a["depth"].sum()).backward()
     (b["image"].sum() + b["depth"].sum()).backward()
     assert g64.xyz.grad.dtype == torch.float64
