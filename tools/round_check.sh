@@ -15,4 +15,5 @@ timeout -k 10 300 python bench.py > "$O/bench.log" 2>&1 || { echo "bench failed"
 tail -1 "$O/bench.log"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > "$O/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$O/prof.log"; exit 1; }
+python3 "$R/tools/timed_kernel_stats.py" "$O/prof/run_kernel_trace.csv" 25 > "$O/kernel_stats_timed.txt" || true
 echo done
