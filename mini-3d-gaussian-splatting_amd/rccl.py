@@ -37,6 +37,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 from typing import List, Sequence, Tuple
 
 import torch
@@ -46,6 +47,11 @@ from . import _native
 NCCL_FLOAT32 = 7
 NCCL_SUM, NCCL_AVG = 0, 4
 HIP_EVENT_DISABLE_TIMING = 0x2
+HIP_ERROR_NOT_READY = 600
+# seconds the self-check collective may take (the first collective of a
+# communicator also sets up its connections); past it the check fails on this
+# rank, and with it the native path on every rank
+SELF_CHECK_TIMEOUT_S = float(os.environ.get("GS_RCCL_CHECK_TIMEOUT", "60"))
 
 
 class _UniqueId(C.Structure):
@@ -83,7 +89,9 @@ def _libs():
         hip.hipEventRecord.argtypes = [vp, vp]
         hip.hipStreamWaitEvent.argtypes = [vp, vp, C.c_uint]
         hip.hipEventDestroy.argtypes = [vp]
-        for f in ("hipEventCreateWithFlags", "hipEventRecord", "hipStreamWaitEvent", "hipEventDestroy"):
+        hip.hipEventQuery.argtypes = [vp]
+        for f in ("hipEventCreateWithFlags", "hipEventRecord", "hipStreamWaitEvent", "hipEventDestroy",
+                  "hipEventQuery"):
             getattr(hip, f).restype = C.c_int
         _LIBS = (rccl, hip)
     return _LIBS
@@ -192,6 +200,10 @@ class RcclComm:
         x = base * float(self.rank + 1)
         ptr = x.data_ptr()
         self.all_reduce(0, [(ptr, cut), (ptr + 4 * cut, n - cut)], avg=True)
+        # bounded: a collective that never completes (a first multi-rank run
+        # whose transport does not work) fails the check instead of hanging
+        # the job; _abort then aborts the communicator (ncclCommAbort)
+        self.wait_done(0, SELF_CHECK_TIMEOUT_S)
         self.wait(0)
         torch.cuda.synchronize(self.device)
         want = base * (self.world + 1) / 2.0
@@ -244,6 +256,19 @@ class RcclComm:
             if group:
                 _check_nccl(rccl, rccl.ncclGroupEnd(), "ncclGroupEnd")
         _check_hip(hip.hipEventRecord(done, coll), "hipEventRecord")
+
+    def wait_done(self, k: int, timeout_s: float) -> None:
+        """The host waits (polling) for range k's collective, at most timeout_s."""
+        deadline = time.monotonic() + timeout_s
+        while True:
+            r = self._hip.hipEventQuery(self._done[k])
+            if r == 0:
+                return
+            if r != HIP_ERROR_NOT_READY:
+                raise RcclError(f"hipEventQuery: hipError {r}")
+            if time.monotonic() > deadline:
+                raise RcclError(f"collective {k} did not complete within {timeout_s:g} s")
+            time.sleep(0.0005)
 
     def wait(self, k: int) -> None:
         """The current stream waits for range k's collective (host does not block)."""

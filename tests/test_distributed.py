@@ -354,3 +354,37 @@ def test_native_comm_decided_by_all_ranks_gloo(fail):
         assert "ncclGetUniqueId" in res[0][1]["fallback_reason"] and "rank 0" in res[1][1]["fallback_reason"]
     if fail == "import":
         assert "import rccl" in res[1][1]["fallback_reason"] and "another rank" in res[0][1]["fallback_reason"]
+
+
+def test_self_check_wait_is_bounded():
+    """A collective that never completes fails the self-check after the
+    timeout (RcclError, so every rank falls back) instead of hanging the job;
+    a completed one returns, and an event error is reported as such."""
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    import importlib
+    pkg = ge.load_package()
+    rccl = importlib.import_module(pkg.__name__ + ".rccl")
+
+    class Hip:
+        def __init__(self, codes):
+            self.codes = list(codes)
+
+        def hipEventQuery(self, ev):
+            return self.codes.pop(0) if len(self.codes) > 1 else self.codes[0]
+
+    comm = object.__new__(rccl.RcclComm)
+    comm._done = [None]
+    comm._hip = Hip([rccl.HIP_ERROR_NOT_READY])
+    t0 = time.monotonic()
+    with pytest.raises(rccl.RcclError, match="did not complete"):
+        comm.wait_done(0, 0.05)
+    assert time.monotonic() - t0 < 5.0
+    comm._hip = Hip([rccl.HIP_ERROR_NOT_READY, rccl.HIP_ERROR_NOT_READY, 0])
+    comm.wait_done(0, 5.0)
+    comm._hip = Hip([rccl.HIP_ERROR_NOT_READY, 719])
+    with pytest.raises(rccl.RcclError, match="hipError 719"):
+        comm.wait_done(0, 5.0)
