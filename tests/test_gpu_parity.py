@@ -193,6 +193,62 @@ def test_needle_gaussians_vs_oracle(pkg, cuda, seed):
     assert not errs, errs
 
 
+def test_degenerate_inputs_vs_oracle(pkg, cuda):
+    """Degenerate parameters through the model path, against the oracle:
+    zero and far-from-unit quaternions (normalize's 1e-12 floor,
+    gaussian_model.py:116-117), opacity logits of +-40 (sigmoid 1.0 and
+    4e-18 in fp32), Gaussians 0.02-0.2 in front of the camera (radius clamp
+    at 50 px, huge Jacobians), behind it (culled), and sub-micro scales
+    (radius_min 0.01: one-pixel rectangles).  Image and projection as
+    everywhere; gradients on every row (rotation per quaternion-norm group,
+    each on its own scale)."""
+    syn = pkg.synthetic
+    n, w, h = 3000, 160, 128
+    sc = syn.make_scene(n, w, h, seed=21)
+    g = torch.Generator().manual_seed(21)
+    sc.rotation[0:50] = 0.0
+    sc.rotation[50:100] *= 1e6
+    sc.rotation[100:150] *= 1e-6
+    sc.opacity[150:200] = 40.0
+    sc.opacity[200:250] = -40.0
+    z = torch.empty(50).uniform_(0.02, 0.2, generator=g)
+    sc.xyz[250:300, 2] = z
+    sc.xyz[250:300, 0] = (torch.rand(50, generator=g) * 2 - 1) * z * math.tan(sc.fovx / 2)
+    sc.xyz[250:300, 1] = (torch.rand(50, generator=g) * 2 - 1) * z * math.tan(sc.fovy / 2)
+    sc.xyz[300:350, 2] = -sc.xyz[300:350, 2]
+    sc.scaling[350:400] = math.log(1e-6)
+    m = syn.to_model(sc, pkg.GaussianModel, cuda)
+    cov = G.oracle().covariance(sc.scaling.numpy(), sc.rotation.numpy())
+    bg = [0.3, 0.2, 0.1]
+    out = pkg.GaussianRenderer().render(Cam(w, h, sc.fovx, sc.fovy), m, pkg.RenderSettings(h, w, torch.tensor(bg)))
+    vis = out["visibility_filter"].cpu()
+    assert not vis[300:350].any() and vis[250:300].any()
+    assert float(out["radii"][250:300][vis[250:300]].max()) == 50.0
+    rng = np.random.default_rng(21)
+    gi, ga, gd = (rng.uniform(-1, 1, s).astype(np.float32) for s in ((3, h, w), (1, h, w), (1, h, w)))
+    L = sum((out[k] * torch.tensor(v, device=cuda)).sum() for k, v in (("image", gi), ("alpha", ga), ("depth", gd)))
+    L.backward()
+    ref = G.oracle().render_backward(_oracle_scene(sc, cov, bg), gi, ga, gd)
+    errs = G.check_image(_outputs(out), ref) + G.check_projection(_outputs(out), ref)
+    ds, dr = G.oracle().covariance_backward(sc.scaling.numpy(), sc.rotation.numpy(), ref["grads"]["cov3d"])
+    op = torch.sigmoid(sc.opacity[:, 0]).numpy()
+    errs += G.check_grad("xyz", _np(m._xyz.grad), ref["grads"]["xyz"])
+    errs += G.check_grad("scaling", _np(m._scaling.grad), ds)
+    # rotation by quaternion norm group, each on its own scale (the 1e-6-norm
+    # rows' gradients are 1e6 x the others'; R is quadratic in the normalised
+    # q, so the zero rows' gradient is zero on both sides)
+    drot = _np(m._rotation.grad)
+    assert np.isfinite(drot).all()
+    rest = np.ones(n, bool)
+    rest[0:150] = False
+    for name, rows in (("rotation zero q", slice(0, 50)), ("rotation |q| 1e6", slice(50, 100)),
+                       ("rotation |q| 1e-6", slice(100, 150)), ("rotation", rest)):
+        errs += G.check_grad(name, drot[rows], dr[rows])
+    errs += G.check_grad("features_dc", _np(m._features_dc.grad)[:, 0], ref["grads"]["color_logits"])
+    errs += G.check_grad("opacity", _np(m._opacity.grad)[:, 0], ref["grads"]["opacity"] * op * (1 - op))
+    assert not errs, errs
+
+
 def test_radix_sort_matches_stable_argsort(pkg, cuda):
     import ctypes as C
     N = pkg._native
