@@ -48,6 +48,10 @@ VALU_PEAK_TFLOPS = 157.3     # FP32 vector, spec (FMA = 2)
 REF_FWD_S_PER_PAIR, REF_FWD_S_PER_CONTRIB = 85e-6, 177e-6
 REF_BIN_S_PER_GAUSSIAN, REF_PROJ_SORT_S_PER_1M = 8.7e-6, 0.40
 REF_BWD_S_PER_CONTRIB_PX = 155e-3 / (256 * 256)
+# workload presets (Gaussians, width, height): BASELINE.json configs[0..2] on the
+# SURVEY 8(d) synthetic distribution, and a 4K frame; C3 is the metric's config
+CONFIGS = {"C1": (5_000, 256, 256), "C2": (100_000, 800, 800), "C3": (1_000_000, 1920, 1080),
+           "4K": (4_000_000, 3840, 2160)}
 
 
 def parse():
@@ -55,9 +59,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)  # (clocks and allocator settle: a 3-step warmup once timed 20 % slow)
-    ap.add_argument("--gaussians", type=int, default=1_000_000)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="C3",
+                    help="workload preset (BASELINE.json configs; C3 = the metric's, the default)")
+    ap.add_argument("--gaussians", type=int, default=None, help="override the preset's Gaussian count")
+    ap.add_argument("--width", type=int, default=None, help="override the preset's image width")
+    ap.add_argument("--height", type=int, default=None, help="override the preset's image height")
     ap.add_argument("--no-optimizer", action="store_true", help="time render fwd+bwd only")
     ap.add_argument("--diag-steps", type=int, default=5, help="untimed steps for the per-stage breakdown")
     # MI355X clocks ramp over the first ~60 ms of load: with 5 warm-up steps the
@@ -74,7 +80,21 @@ def parse():
                     help="nccl (= RCCL over xGMI) for the driver; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--force-dist", action="store_true",
                     help="init the process group and all-reduce even at world size 1 (rehearses the RCCL path)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    n0, w0, h0 = CONFIGS[a.config]
+    a.gaussians = n0 if a.gaussians is None else a.gaussians
+    a.width = w0 if a.width is None else a.width
+    a.height = h0 if a.height is None else a.height
+    return a
+
+
+def workload_name(n: int, w: int, h: int) -> str:
+    """The BASELINE.json config these sizes are (C1 / C2 / C3 / 4K), or
+    "custom": the bench line names its own workload, whatever flags set it."""
+    for k, v in CONFIGS.items():
+        if v == (n, w, h):
+            return k
+    return "custom"
 
 
 def view_matrix(rank: int) -> torch.Tensor:
@@ -297,15 +317,17 @@ def main():
             psnr = {"db": round(10 * math.log10(1.0 / mse), 2) if mse > 0 else None,
                     "mse": mse, "max_abs_err": float(np.abs(err).max()),
                     "pixels_over_1e-4": int((np.abs(err).max(axis=0) > 1e-4).sum()),
-                    "ref": "oracle/gs_oracle.c on the same C3 frame (CPU restatement of renderer.py, "
+                    "ref": "oracle/gs_oracle.c on the same frame (CPU restatement of renderer.py, "
                            "pinned to the reference's own outputs); db None = bit-identical images"}
+        wl = workload_name(n, W, H)
         line = {
             "metric": METRIC, "value": round(mpix, 3), "unit": "Mpix/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "spinup_steps": a.spinup_steps, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "C3: 1M synthetic Gaussians (SURVEY 8d), 1920x1080, 16x16 tiles, "
+            "config": {"workload": f"{wl}: {n:,} synthetic Gaussians (SURVEY 8d), {W}x{H}, 16x16 tiles, "
                                    "render fwd+bwd" + (" + grad all-reduce" if reducer is not None else "")
                                    + ("" if opt is None else " + Adam step"),
+                       "preset": wl,
                        "gaussians": n, "width": W, "height": H, "views_per_step": world,
                        "parallelism": f"dp{world} (one view per GPU)", "visible": M, "tile_touches": T,
                        "records_consumed": R, "evaluated_pairs": E, "contributing_pairs": Cc},
@@ -422,7 +444,7 @@ def cpu_limit():
 
 def cpu_baseline(scene, W, H, cot, threads):
     """Oracle (C restatement of the reference render path) fwd+bwd on the
-    host cores for the same C3 frame: one frame per thread count of a sweep
+    host cores for the same frame: one frame per thread count of a sweep
     (16, 32, 64, 128, 256, capped by the CPUs this process may use, cgroup
     quota included; `threads` > 0 adds that count), the fastest reported, then
     one frame on one core.  Bounded: ~1 s per multi-thread frame, ~10 s on one
@@ -452,7 +474,7 @@ def cpu_baseline(scene, W, H, cot, threads):
     dt1 = time.perf_counter() - t0
     threads, dt = best
     return {"value": round(H * W / dt / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"one full C3 frame ({W}x{H}, {scene.xyz.shape[0]} Gaussians) fwd+bwd per thread count, "
+            "sample": f"one full {workload_name(scene.xyz.shape[0], W, H)} frame ({W}x{H}, {scene.xyz.shape[0]} Gaussians) fwd+bwd per thread count, "
                       f"oracle/gs_oracle.c with OpenMP; fastest x{threads} ({dt:.2f} s), 1 core ({dt1:.2f} s)",
             "thread_sweep_mpix_s": sweep, "cpu_limit": info,
             "one_core": {"value": round(H * W / dt1 / 1e6, 4), "unit": "Mpix/s", "cores": 1},

@@ -31,13 +31,11 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 16
+#define GS_ABI_VERSION 17
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 4096      /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
                                  of at least max(W, H) renders the same as any larger one (one tile
                                  holds the image), so callers clamp to max(W, H) */
-#define GS_DENSE_MAX_TILE 256 /* above this tile edge the blend backward sums gradients per Gaussian
-                                 with fp32 atomics (gs_partial_groups returns 0) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
                                  edge L holds gs_tile_quads(L) = ceil(L/8)^2 of them (edge cells
                                  clipped to the tile); one 64-lane wave renders one cell */
@@ -249,7 +247,9 @@ typedef struct gs_blend_fwd_args {
   float *depth;                 /* [H,W]   */
   float *pix_acc;               /* [H*W,4] */
   float *pix_state;             /* [H*W,2] */
-  uint64_t *live_bits;          /* [gs_tile_quads(tile_size), live_words]: see gs_blend_live_words */
+  uint64_t *live_bits;          /* [gs_tile_quads(tile_size), live_words]: see gs_blend_live_words;
+                                   NULL: none written (a caller's memory budget for large tiles; the
+                                   backward then replays every entry of a cell's evaluated prefix) */
   int64_t live_words;
   uint32_t *pair_counts;        /* [H*W] or NULL: each pixel's contributing pairs (c > 0), the
                                    work counter C of SURVEY 8(d); measurement only */
@@ -267,14 +267,13 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
 size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles);
 /* Cells per tile: ceil(tile_size / 8)^2 (4 for the default 16); 0 if out of range. */
 int32_t gs_tile_quads(int32_t tile_size);
-/* Gradient partials gs_blend_backward writes per list entry (G below): one
- * per 8x8 cell, gs_tile_quads(tile_size) (4 for the default 16x16 tile), up
- * to GS_DENSE_MAX_TILE.  Above it 0: a dense [T, G] partial buffer would grow
- * with (L/8)^2, so the backward adds each (entry, cell)'s sums into the
- * Gaussian's row of an [n, GS_PAIR_GRAD_FLOATS] buffer with fp32 atomics
- * (pair_grads = that buffer, zeroed by the caller; slot_live unused; the
- * projection backward reads it as grad_sums and skips the gather).  0 also
- * if out of range. */
+/* Gradient partials a one-batch gs_blend_backward writes per list entry: one
+ * per 8x8 cell, gs_tile_quads(tile_size) (4 for the default 16x16 tile); 0 if
+ * out of range.  A caller whose [T, cells] partial buffer would not fit its
+ * memory budget (large tiles: (L/8)^2 cells) replays the cells in batches
+ * (gs_blend_bwd_args.cell_begin / cell_count), summing each batch with
+ * gs_gather_partials(accumulate) before the next: bounded memory, the same
+ * fixed summation order on every run (deterministic at every tile size). */
 int32_t gs_partial_groups(int32_t tile_size);
 
 /* ---- Backward of the blend -------------------------------------------
@@ -286,7 +285,10 @@ int32_t gs_partial_groups(int32_t tile_size);
  * slot_live[G e + q] = 1; G = gs_partial_groups(tile_size), e = the entry's
  * gradient slot (pair_offset[g] + its tile's index in g's rectangle).  One
  * 64-lane workgroup per (tile, cell), and the group is the cell.  Groups
- * that did not replay the entry write nothing.  No atomics: deterministic. */
+ * that did not replay the entry write nothing.  No atomics: deterministic.
+ * A launch replays the cells [cell_begin, cell_begin + cell_count) of every
+ * tile (cell_count 0 with cell_begin 0: all of them); G is then cell_count
+ * and group q - cell_begin holds cell q's partial. */
 typedef struct gs_blend_bwd_args {
   gs_camera cam;
   int32_t tiles_x, tiles_y;
@@ -300,10 +302,11 @@ typedef struct gs_blend_bwd_args {
   const float *g_depth;         /* [H,W] or NULL */
   const uint64_t *live_bits;    /* the forward's liveness bitmap */
   int64_t live_words;
-  float *pair_grads;            /* [T, G, GS_PARTIAL_STRIDE], G = gs_partial_groups(cam.tile_size);
-                                   G = 0: [n, GS_PAIR_GRAD_FLOATS] sums, zeroed by the caller */
-  uint8_t *slot_live;           /* [T, G], zeroed by the caller (or gs_tile_ranges); unused when G = 0 */
+  float *pair_grads;            /* [T, G, GS_PARTIAL_STRIDE], G = the batch's cell_count */
+  uint8_t *slot_live;           /* [T, G], zeroed by the caller (or gs_tile_ranges) */
   int32_t num_pairs;            /* T, the entries of sorted_gauss: tile ranges are clamped to it */
+  int32_t cell_begin;           /* the batch's first cell (0) */
+  int32_t cell_count;           /* the batch's cells (0: gs_tile_quads(tile_size), the whole tile) */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
 
@@ -325,8 +328,9 @@ typedef struct gs_project_bwd_args {
   const uint32_t *pair_offset;
   const uint32_t *order;       /* [n] permutation to walk the Gaussians in, or NULL: index order
                                   (slots are numbered in index order, so NULL reads them coalesced) */
-  const float *pair_grads;     /* [T,G,GS_PARTIAL_STRIDE] (gs_partial_groups); may be NULL when T == 0;
-                                  G = 0: the blend backward's [n, 10] sums (also passed as grad_sums) */
+  const float *pair_grads;     /* [T,G,GS_PARTIAL_STRIDE] (G = partial_groups), summed into grad_sums
+                                  first; NULL: no blend gradient (T == 0), or -- with grad_sums --
+                                  the sums are already there (gs_gather_partials, cell batches) */
   const float *g_means2d;      /* [n,2] or NULL */
   const float *g_conics;       /* [n,4] or NULL */
   float *d_xyz;                /* [n,3] */
@@ -337,10 +341,16 @@ typedef struct gs_project_bwd_args {
   float *d_opacity;            /* [n]   */
   float *d_sh_rest;            /* [n,15,3] contiguous, written when g.sh_degree > 0 (zeros past the degree) */
   const uint8_t *slot_live;    /* [T,G] from gs_blend_backward; required with pair_grads */
-  float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS] scratch (g's partials summed); with pair_grads;
-                                  G = 0: the sums themselves (read, not written) */
+  float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS]: g's partials summed (written first when
+                                  pair_grads is given, else read as is); NULL: no blend gradient */
+  int32_t partial_groups;      /* G of pair_grads / slot_live: the blend backward's cell_count */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
+/* The gather alone: grad_sums[g] = (accumulate ? grad_sums[g] : 0) + the sum
+ * of g's partials in pair_grads / slot_live (partial_groups per slot), for a
+ * blend backward run in cell batches: batch b's sums are added after batch
+ * b - 1's, a fixed order.  Reads vis, rects, pair_offset, g.n. */
+gs_status gs_gather_partials(const gs_project_bwd_args *a, int32_t accumulate, gs_stream_t stream);
 
 /* ---- Adam step over several parameter tensors, one launch -----------------
  * SURVEY 8(f) row 1 (fused Adam), the optimizer the reference builds in

@@ -22,13 +22,12 @@ LIB_PATH = os.environ.get("GS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 
 GS_DEFAULT_TILE = 16  # renderer.py:24
 GS_MAX_TILE = 4096
-GS_DENSE_MAX_TILE = 256  # above: gradient sums per Gaussian by fp32 atomics (gs_partial_groups == 0)
 GS_QUAD = 8  # 8x8 pixel cells per wave, ceil(tile/8)^2 per tile (gs_tile_quads)
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 16
+GS_ABI_VERSION = 17
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -92,7 +91,7 @@ class GsBlendBwdArgs(C.Structure):
         ("sorted_gauss", _vp), ("records", _vp), ("pix_acc", _vp),
         ("pix_state", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp),
         ("live_bits", _vp), ("live_words", C.c_int64), ("pair_grads", _vp), ("slot_live", _vp),
-        ("num_pairs", C.c_int32),
+        ("num_pairs", C.c_int32), ("cell_begin", C.c_int32), ("cell_count", C.c_int32),
     ]
 
 
@@ -102,7 +101,7 @@ class GsProjectBwdArgs(C.Structure):
         ("rects", _vp), ("pair_offset", _vp), ("order", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
         ("g_conics", _vp), ("d_xyz", _vp), ("d_cov3d", _vp), ("d_scaling", _vp),
         ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
-        ("slot_live", _vp), ("grad_sums", _vp),
+        ("slot_live", _vp), ("grad_sums", _vp), ("partial_groups", C.c_int32),
     ]
 
 
@@ -160,7 +159,7 @@ EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
     "gs_tile_ranges", "gs_blend_live_words", "gs_tile_quads", "gs_partial_groups", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-    "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
+    "gs_gather_partials", "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
     "gs_densify_workspace_bytes", "gs_densify_count", "gs_densify_emit",
 )
 
@@ -197,6 +196,7 @@ def _declare(lib):
     lib.gs_blend_forward.argtypes = [P(GsBlendFwdArgs), _vp]
     lib.gs_blend_backward.argtypes = [P(GsBlendBwdArgs), _vp]
     lib.gs_project_backward.argtypes = [P(GsProjectBwdArgs), _vp]
+    lib.gs_gather_partials.argtypes = [P(GsProjectBwdArgs), C.c_int32, _vp]
     lib.gs_adam_step.argtypes = [P(GsAdamArgs), _vp]
     lib.gs_loss_workspace_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32]
     lib.gs_loss_workspace_bytes.restype = C.c_size_t
@@ -208,7 +208,7 @@ def _declare(lib):
     lib.gs_densify_emit.argtypes = [P(GsDensifyArgs), _vp]
     for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_count", "gs_bin_emit",
               "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-              "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
+              "gs_gather_partials", "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
         getattr(lib, f).restype = C.c_int
 
 

@@ -1174,8 +1174,9 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
   const float fx = (float)px, fy = (float)py;
   const float4 *recs = reinterpret_cast<const float4 *>(a.records);
   // liveness word of (this batch, this cell): see gs_blend_live_words
-  uint64_t *live = a.live_bits + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile;
-  const uint64_t live_left = (uint64_t)a.live_words - (start / 64u + (uint32_t)tile);
+  // (no bitmap: the caller's budget; the backward then replays every entry)
+  uint64_t *live = a.live_bits ? a.live_bits + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile : nullptr;
+  const uint64_t live_left = a.live_bits ? (uint64_t)a.live_words - (start / 64u + (uint32_t)tile) : 0u;
   float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
   if (start + (uint32_t)lane < end) {
     const uint32_t gid = a.sorted_gauss[start + lane];
@@ -1313,13 +1314,12 @@ __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
 }
 
 
-// kSums: tiles above GS_DENSE_MAX_TILE (gs_partial_groups == 0): a per-(entry,
-// cell) partial buffer would need T x (L/8)^2 x 40 B, so each (entry, cell)'s
-// sums go straight into the Gaussian's [n, 10] row of pair_grads with fp32
-// atomics (bounded memory; reproducible to rounding only; 4x the partial
-// path's cost per sum -- tools/variants/README.md -- on tile sizes no
-// performance path uses).
-template <bool kT16, bool kSums>
+// One launch replays the cells [cell_begin, cell_begin + cell_count) of every
+// tile (the caller's batch: all of them unless a tile's cells would make the
+// [T, cells] partial buffer too large; each batch's partials are summed by
+// gs_gather_partials before the next batch overwrites them).  kT16: the
+// default tile, one batch of its four cells.
+template <bool kT16>
 __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
@@ -1327,11 +1327,13 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   // 384 B instead of a word's 3 KB, for occupancy (LDS bounds it)
   __shared__ float2 s_wrec[kBwdGroup * 6];
   const CellGeom cg(kT16 ? GS_DEFAULT_TILE : a.cam.tile_size);
-  const int ncell = cg.cells();
-  int tile, quad;
+  const int ncell = kT16 ? cg.cells() : a.cell_count;  // partial groups of this batch
+  const int cell0 = kT16 ? 0 : a.cell_begin;
+  int tile, qb;
   uint32_t start, lend;
-  cell_tile(blockIdx.x, ncell, a.ranges, a.tiles_x * a.tiles_y, (uint32_t)a.num_pairs, tile, quad, start, lend);
+  cell_tile(blockIdx.x, ncell, a.ranges, a.tiles_x * a.tiles_y, (uint32_t)a.num_pairs, tile, qb, start, lend);
   if (tile >= a.tiles_x * a.tiles_y) return;
+  const int quad = cell0 + qb;  // the cell in its tile; qb its partial group
   const int lane = threadIdx.x;
   const uint32_t tx = (uint32_t)(tile % a.tiles_x), ty = (uint32_t)(tile / a.tiles_x);
   const int cx0 = (quad % cg.QX) * 8, cy0 = (quad / cg.QX) * 8;  // the cell in its tile
@@ -1347,9 +1349,13 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   // (2) speculatively every word-0 entry's record, not only the live ones.
   // Lanes outside the image / past the list read valid dummies (pixel 0,
   // entry 0), never used.
+  // no bitmap (the caller's memory budget): every entry counts as live, and
+  // the per-lane tests decide alone (slower, the same sums)
   const unsigned long long *lw =
-      reinterpret_cast<const unsigned long long *>(a.live_bits) + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile;
-  const unsigned long long w0 = lw[0];
+      a.live_bits ? reinterpret_cast<const unsigned long long *>(a.live_bits) + (size_t)quad * a.live_words +
+                        start / 64u + (uint32_t)tile
+                  : nullptr;
+  const unsigned long long w0 = lw ? lw[0] : ~0ull;
   const uint32_t gid0 = a.sorted_gauss[start + (uint32_t)lane < lend ? start + (uint32_t)lane : 0u];
   const size_t HW = (size_t)W * H;
   const size_t p = inside ? (size_t)py * W + px : 0;
@@ -1399,7 +1405,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
   const uint32_t nwords = (wstop + 63u) >> 6;
   // liveness word wd of this quadrant, cut at wstop (bits past it were never written)
   auto live_word = [&](uint32_t wd) -> unsigned long long {
-    const unsigned long long w = wd == 0 ? w0 : lw[wd];
+    const unsigned long long w = wd == 0 ? w0 : (lw ? lw[wd] : ~0ull);
     // (readfirstlane returns int: widen through uint32_t, never sign-extend)
     const unsigned long long m =
         ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32) |
@@ -1408,12 +1414,9 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     return rem < 64u ? m & ((1ull << rem) - 1ull) : m;
   };
   // lane l gathers the record of entry 64 wd + l when that entry is live here
-  // (kSums: and keeps its Gaussian id for the atomic sums)
-  uint32_t gcur = gid0, gnx = 0u;
   auto fetch = [&](uint32_t wd, unsigned long long m) {
     if ((m >> lane) & 1ull) {
       const uint32_t gid = a.sorted_gauss[start + 64u * wd + (uint32_t)lane];
-      gnx = gid;
       r0 = recs[3 * (size_t)gid];
       r1 = recs[3 * (size_t)gid + 1];
       r2 = recs[3 * (size_t)gid + 2];
@@ -1490,24 +1493,11 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       float g4 = __builtin_fmaf(by, __builtin_fmaf(by, S0, 2.f * Soy), Soyy);
       Sx = oct_sum(Sx); Sy = oct_sum(Sy); g2 = oct_sum(g2); g3 = oct_sum(g3); g4 = oct_sum(g4);
       g5 = oct_sum(g5); g6 = oct_sum(g6); g7 = oct_sum(g7); g8 = oct_sum(g8); g9 = oct_sum(g9);
-      if constexpr (kSums) {
-        // the entry's 10 sums into its Gaussian's row: lane 8j + c adds
-        // component c, lanes 8j, 8j + 1 components 8, 9 (no-return atomics)
-        const uint32_t gid = __float_as_uint(s_wrec[6 * e + 5].y);
-        const float q00 = ia.z, qo = ib.x, q11 = ia.w;
-        const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
-        const float v = col == 0 ? g0 : col == 1 ? g1 : col == 2 ? g2 : col == 3 ? g3 : col == 4 ? g4
-                      : col == 5 ? g5 : col == 6 ? g6 : g7;
-        float *dst = a.pair_grads + (size_t)gid * GS_PAIR_GRAD_FLOATS;
-        (void)__hip_atomic_fetch_add(dst + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (col < 2)
-          (void)__hip_atomic_fetch_add(dst + 8 + col, col ? g9 : g8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        (void)slot;
-      } else if (col == 0) {
+      if (col == 0) {
         const float q00 = ia.z, qo = ib.x, q11 = ia.w;
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
-        const size_t sq = (size_t)slot * (uint32_t)ncell + (uint32_t)quad;
+        const size_t sq = (size_t)slot * (uint32_t)ncell + (uint32_t)qb;
         // (dense 40-B partials, 8-B aligned: f4_u8)
         float *out = a.pair_grads + sq * GS_PARTIAL_STRIDE;
         *reinterpret_cast<f4_u8 *>(out) = f4_u8{g0, g1, g2, g3};
@@ -1532,7 +1522,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     // this word's records stay in registers (staged chunk by chunk below)
     // while the next word's are fetched into r0..r2 (staging a whole word's
     // records, 3 KB of LDS, cost occupancy: -13 us when chunked)
-    const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), kSums ? __uint_as_float(gcur) : 0.f);
+    const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
     const unsigned long long simple_w = __builtin_amdgcn_ballot_w64(mine && simple_entry(r0, r1));
     const unsigned long long mnext = wd + 1u < nwords ? live_word(wd + 1u) : 0ull;
     fetch(wd + 1u, mnext);  // in flight while this word replays
@@ -1632,7 +1622,6 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     };
     if ((simple_w & mcur) == mcur) run_word(std::true_type{}); else run_word(std::false_type{});
     mcur = mnext;
-    gcur = gnx;
   }
 }
 
@@ -1740,8 +1729,10 @@ __device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint3
   }
 }
 
+// accumulate: grad_sums = grad_sums + this batch's sums (the cell batches of
+// one backward, added in batch order: deterministic), else grad_sums = them.
 template <int QL, int HL, int kNG = 0>  // kNG > 0: the partial groups per slot at compile time (else ng)
-__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng_rt) {
+__global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng_rt, int accumulate) {
   constexpr int LPG = QL * HL;
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const int g = (int)(t / LPG);
@@ -1749,8 +1740,16 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, 
   gather_slots<QL, HL, kNG>(a, kNG > 0 ? (uint32_t)kNG : ng_rt, t, acc);
   if ((t % LPG) == 0 && g < a.g.n) {
     float2 *out = reinterpret_cast<float2 *>(a.grad_sums) + (size_t)g * kF2;
+    if (accumulate) {
 #pragma unroll
-    for (int k = 0; k < kF2; ++k) out[k] = acc[k];
+      for (int k = 0; k < kF2; ++k) {
+        const float2 o = out[k];
+        out[k] = make_float2(o.x + acc[k].x, o.y + acc[k].y);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kF2; ++k) out[k] = acc[k];
+    }
   }
 }
 
@@ -1981,7 +1980,7 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
   project_bwd_one<kHot>(a, g, [&](float acc[GS_PAIR_GRAD_FLOATS]) {
 #pragma unroll
     for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
-    if (kHot || a.pair_grads) {  // g's partials summed (k_gather_slots)
+    if (kHot || a.grad_sums) {  // g's partials summed (k_gather_slots)
       const float2 *gs = reinterpret_cast<const float2 *>(a.grad_sums) + (size_t)g * kF2;
 #pragma unroll
       for (int k = 0; k < kF2; ++k) {
@@ -2078,17 +2077,13 @@ int cells_per_tile(int tile_size) {
   return qx * qx;
 }
 
-// gradient partials gs_blend_backward writes per list entry: one per cell
-// (a wave combining a tile's cells wrote fewer and replayed slower:
-// tools/variants/README.md)
-int partial_groups(int tile_size) { return tile_size > GS_DENSE_MAX_TILE ? 0 : cells_per_tile(tile_size); }
 
 // tile_size in range, image non-empty, tile coordinates fit 12 bits
 bool cam_ok(const gs_camera &c) {
   if (c.tile_size < 1 || c.tile_size > GS_MAX_TILE || c.image_width <= 0 || c.image_height <= 0) return false;
   return div_up(c.image_width, c.tile_size) <= GS_MAX_TILES_AXIS && div_up(c.image_height, c.tile_size) <= GS_MAX_TILES_AXIS;
 }
-const char *kCamMsg = "%s: tile_size must be in [1, 256], the image non-empty with at most 4096 tiles per axis";
+const char *kCamMsg = "%s: tile_size must be in [1, 4096], the image non-empty with at most 4096 tiles per axis";
 
 // A Gaussian's rectangle is at most 2 floor(r) + 1 <= 2 floor(radius_max) + 1
 // pixels wide (renderer.py:278-293), clipped to the image: its tile width
@@ -2262,7 +2257,9 @@ int32_t gs_tile_quads(int32_t tile_size) {
 }
 
 int32_t gs_partial_groups(int32_t tile_size) {
-  return (tile_size < 1 || tile_size > GS_MAX_TILE) ? 0 : partial_groups(tile_size);
+  // one partial per 8x8 cell (a wave combining a tile's cells wrote fewer and
+  // replayed slower: tools/variants/README.md)
+  return (tile_size < 1 || tile_size > GS_MAX_TILE) ? 0 : cells_per_tile(tile_size);
 }
 
 size_t gs_blend_live_words(int32_t num_pairs, int32_t num_tiles) {
@@ -2276,7 +2273,7 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   if (!tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_forward");
   if (!a->ranges || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_acc || !a->pix_state ||
-      !a->live_bits || a->live_words <= 0 || (a->num_pairs > 0 && !a->sorted_gauss))
+      (a->live_bits && a->live_words <= 0) || (a->num_pairs > 0 && !a->sorted_gauss))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_forward");
   if (a->num_pairs < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative num_pairs", "gs_blend_forward");
   hipStream_t s = (hipStream_t)stream;
@@ -2298,22 +2295,49 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_backward");
   if (!a->ranges || !a->sorted_gauss || !a->records || !a->pix_acc || !a->pix_state || !a->g_image ||
-      !a->pair_grads || (!a->slot_live && partial_groups(a->cam.tile_size) > 0) || !a->live_bits ||
-      a->live_words <= 0)
+      !a->pair_grads || !a->slot_live || (a->live_bits && a->live_words <= 0))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_backward");
   if (a->num_pairs < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative num_pairs", "gs_blend_backward");
+  const int cells = cells_per_tile(a->cam.tile_size);
+  gs_blend_bwd_args b = *a;
+  if (b.cell_count == 0 && b.cell_begin == 0) b.cell_count = cells;  // (0: every cell, one batch)
+  if (b.cell_begin < 0 || b.cell_count < 1 || b.cell_begin + b.cell_count > cells)
+    return fail(GS_ERR_INVALID_ARG, "%s: the cell batch [cell_begin, cell_begin + cell_count) must lie in "
+                "[0, gs_tile_quads(tile_size))", "gs_blend_backward");
   hipStream_t s = (hipStream_t)stream;
-  const int num_tiles = a->tiles_x * a->tiles_y;
+  const int num_tiles = b.tiles_x * b.tiles_y;
   if (num_tiles <= 0) return GS_OK;
-  const long long blocks = (long long)div_up(num_tiles, 8) * 8LL * cells_per_tile(a->cam.tile_size);
+  const long long blocks = (long long)div_up(num_tiles, 8) * 8LL * b.cell_count;
   if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_backward");
-  if (a->cam.tile_size == GS_DEFAULT_TILE)
-    k_blend_bwd<true, false><<<(unsigned)blocks, kWave, 0, s>>>(*a);
-  else if (partial_groups(a->cam.tile_size) > 0)
-    k_blend_bwd<false, false><<<(unsigned)blocks, kWave, 0, s>>>(*a);
+  if (b.cam.tile_size == GS_DEFAULT_TILE && b.cell_count == cells)
+    k_blend_bwd<true><<<(unsigned)blocks, kWave, 0, s>>>(b);
   else
-    k_blend_bwd<false, true><<<(unsigned)blocks, kWave, 0, s>>>(*a);
+    k_blend_bwd<false><<<(unsigned)blocks, kWave, 0, s>>>(b);
   return check_launch("gs_blend_backward");
+}
+
+namespace {
+gs_status launch_gather(const gs_project_bwd_args *a, int accumulate, hipStream_t s) {
+  const uint32_t ng = (uint32_t)a->partial_groups;
+  if (ng == 1)
+    k_gather_slots<1, kGatherHL1><<<div_up((long long)kGatherHL1 * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng, accumulate);
+  else if (ng == 2)
+    k_gather_slots<2, 2><<<div_up(4LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng, accumulate);
+  else if (ng == 4)  // the default tile's four cells
+    k_gather_slots<4, 2, 4><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng, accumulate);
+  else
+    k_gather_slots<4, 2><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng, accumulate);
+  return check_launch("gs_gather_partials");
+}
+}  // namespace
+
+gs_status gs_gather_partials(const gs_project_bwd_args *a, int32_t accumulate, gs_stream_t stream) {
+  if (!a) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_gather_partials");
+  if (a->g.n <= 0) return GS_OK;
+  if (!a->pair_grads || !a->slot_live || !a->grad_sums || !a->vis || !a->rects || !a->pair_offset ||
+      a->partial_groups < 1)
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer or partial_groups < 1", "gs_gather_partials");
+  return launch_gather(a, accumulate, (hipStream_t)stream);
 }
 
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) {
@@ -2323,24 +2347,17 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   if (!a->g.xyz || !a->g.color_logits || !a->means2d || !a->conics || !a->vis || !a->rects ||
       !a->pair_offset || !a->d_xyz || !a->d_color_logits || !a->d_opacity ||
       (raw ? (!a->g.scaling || !a->g.rotation || !a->d_scaling || !a->d_rotation) : !a->d_cov3d) ||
-      (a->pair_grads && (!a->grad_sums || (!a->slot_live && partial_groups(a->cam.tile_size) > 0))))
+      (a->pair_grads && (!a->grad_sums || !a->slot_live || a->partial_groups < 1)))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_project_backward");
   if (a->g.sh_degree < 0 || a->g.sh_degree > 3 || (a->g.sh_degree > 0 && (!a->g.sh_rest || !a->d_sh_rest)))
     return fail(GS_ERR_INVALID_ARG, "%s: sh_degree must be 0..3, with sh_rest and d_sh_rest when > 0",
                 "gs_project_backward");
   if (a->pair_grads && !cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_project_backward");
   hipStream_t s = (hipStream_t)stream;
-  const bool hot = a->pair_grads && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
-  if (a->pair_grads && partial_groups(a->cam.tile_size) > 0) {  // (0: the sums are in grad_sums already)
-    const uint32_t ng = (uint32_t)partial_groups(a->cam.tile_size);
-    if (ng == 1)
-      k_gather_slots<1, kGatherHL1><<<div_up((long long)kGatherHL1 * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
-    else if (ng == 2)
-      k_gather_slots<2, 2><<<div_up(4LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
-    else if (ng == 4)  // the default tile's four cells
-      k_gather_slots<4, 2, 4><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
-    else
-      k_gather_slots<4, 2><<<div_up(8LL * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng);
+  const bool hot = a->grad_sums && !a->g_means2d && !a->g_conics && !a->g.cov3d && a->g.sh_degree == 0 && !a->order;
+  if (a->pair_grads) {  // (NULL with grad_sums: the sums are there already, gs_gather_partials)
+    gs_status st = launch_gather(a, 0, s);
+    if (st) return st;
   }
   if (hot)
     k_project_bwd<true><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);

@@ -51,6 +51,13 @@ def _agreement(dist, group, device):
     return agree
 
 
+def _comm_key(dist, group, device) -> tuple:
+    """The (process group, device) key of _NATIVE_COMMS / NATIVE_STATUS."""
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    return (id(group if group is not None else dist.group.WORLD), str(device))
+
+
 def _native_comm(dist, group, factory=None, device=None):
     """The process group's RcclComm on the current device, or None -- decided
     by all ranks together (rccl.RcclComm: every construction step that can
@@ -64,7 +71,7 @@ def _native_comm(dist, group, factory=None, device=None):
     global _ATEXIT
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
-    key = (id(group if group is not None else dist.group.WORLD), str(device))
+    key = _comm_key(dist, group, device)
     if key not in _NATIVE_COMMS:
         coll_dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
         agree = _agreement(dist, group, coll_dev)
@@ -98,8 +105,11 @@ def _native_comm(dist, group, factory=None, device=None):
     return _NATIVE_COMMS[key]
 
 
-def native_status() -> Optional[dict]:
-    """The last native-communicator decision (None before any)."""
+def native_status(key=None) -> Optional[dict]:
+    """The native-communicator decision for `key` (_comm_key(dist, group,
+    device)); without a key the most recent one.  None before any."""
+    if key is not None:
+        return NATIVE_STATUS.get(key)
     return next(reversed(NATIVE_STATUS.values())) if NATIVE_STATUS else None
 
 
@@ -172,7 +182,9 @@ class GradAllReduce:
         if (self._avg and mode != "0") or (mode == "force" and torch.cuda.is_available()
                                             and hasattr(dist, "is_initialized") and dist.is_initialized()):
             self._native = _native_comm(dist, group)
-            self.native_status = dict(native_status())
+            # this group's own decision (a cached communicator's, not the
+            # newest entry: another group may have been added since)
+            self.native_status = dict(native_status(_comm_key(dist, group, None)))
             if self._native is not None:
                 self._avg = True  # ncclAvg forms the mean (no division after the reduction)
 

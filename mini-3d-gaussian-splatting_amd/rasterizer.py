@@ -60,9 +60,9 @@ class CameraParams:
 
     @property
     def groups(self) -> int:
-        """Gradient partials the blend backward writes per list entry
-        (gs_partial_groups): one per cell, 4 at the default tile; 0 above
-        GS_DENSE_MAX_TILE (per-Gaussian sums by atomics instead)."""
+        """Gradient partials a one-batch blend backward writes per list entry
+        (gs_partial_groups): one per cell, 4 at the default tile.  Large tiles
+        may replay their cells in batches (cell_batch)."""
         return _partial_groups(self.tile_size)
 
     def to_struct(self) -> N.GsCamera:
@@ -94,6 +94,34 @@ def _partial_groups(tile_size: int) -> int:
     if g is None:
         g = _GROUPS[tile_size] = int(N.load().gs_partial_groups(int(tile_size)))
     return g
+
+
+# Memory budgets for tiles of many 8x8 cells (the default tile's four cells
+# never batch, the performance path): the backward's [T, G] partials + flags
+# per cell batch, and the forward's [cells, live_words] liveness bitmap
+# (above it none is written and the backward replays every entry).
+PARTIAL_BUDGET_BYTES = int(os.environ.get("GS_PARTIAL_BUDGET", str(2 << 30)))
+LIVE_BUDGET_BYTES = int(os.environ.get("GS_LIVE_BUDGET", str(1 << 30)))
+_ALWAYS_ONE_BATCH = 4  # cells
+
+
+def cell_batch(cells: int, entries: int) -> int:
+    """Cells per blend-backward batch for a frame of `entries` list entries:
+    every cell at once unless the [entries, cells] partials (40 B) and flags
+    (1 B) would exceed PARTIAL_BUDGET_BYTES; batches are summed in order by
+    gs_gather_partials (deterministic, bounded memory)."""
+    per = 41 * max(int(entries), 1)
+    if cells <= _ALWAYS_ONE_BATCH or cells * per <= PARTIAL_BUDGET_BYTES:
+        return cells
+    return max(1, min(cells, PARTIAL_BUDGET_BYTES // per))
+
+
+def live_bitmap_bytes(lib, cells: int, entries: int, num_tiles: int) -> int:
+    """Bytes of the forward's liveness bitmap, or 0 when it exceeds
+    LIVE_BUDGET_BYTES (then none is written; ADVICE r04: at 1080p a tile of
+    1920 px holds 57,600 cells, ~7 GB of bitmap for 1M Gaussians)."""
+    nbytes = 8 * cells * int(lib.gs_blend_live_words(int(entries), int(num_tiles)))
+    return nbytes if cells <= _ALWAYS_ONE_BATCH or nbytes <= LIVE_BUDGET_BYTES else 0
 
 
 def _rows(t: torch.Tensor, cols: int) -> Tuple[torch.Tensor, int]:
@@ -165,7 +193,7 @@ def _check_inputs(xyz: torch.Tensor):
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
     __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_acc",
-                 "pix_state", "live_bits", "big", "M", "T", "slot_live")
+                 "pix_state", "live_bits", "big", "M", "T", "slot_live", "groups")
 
 
 _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess)
@@ -315,12 +343,12 @@ def window_holds(window, zmin_bits: int, zmax_bits: int) -> bool:
 def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cam: CameraParams, dev):
     """One byte buffer for T <= cap entries: tile keys + Gaussian ids
     (ping-pong, 16 B/entry), the tile sort's workspace, the liveness bitmap
-    (cells x gs_blend_live_words) and the backward's slot flags (partial
-    groups B/entry)."""
+    (cells x gs_blend_live_words, within LIVE_BUDGET_BYTES) and the backward's
+    slot flags (the first cell batch's groups, B/entry)."""
     nbytes = (16 * cap + 255) // 256 * 256
     nbytes += (int(lib.gs_radix_sort_workspace_bytes(cap)) + 255) // 256 * 256
-    nbytes += 8 * cam.cells * int(lib.gs_blend_live_words(cap, num_tiles))
-    nbytes += (cam.groups * cap + 255) // 256 * 256  # the backward's slot flags (zeroed by gs_tile_ranges)
+    nbytes += live_bitmap_bytes(lib, cam.cells, cap, num_tiles)
+    nbytes += (cell_batch(cam.cells, cap) * cap + 255) // 256 * 256  # slot flags (zeroed by gs_tile_ranges)
     return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
 
 
@@ -329,7 +357,7 @@ class _TileLayout:
     tile keys and Gaussian ids (ping-pong), the tile sort's workspace, the
     liveness bitmap (stride live_words, sized for `cap` entries)."""
     __slots__ = ("big", "cap", "p_tk", "p_tv", "p_ws", "ws_bytes", "o_live", "p_live", "live_words", "bits",
-                 "o_flags")
+                 "o_flags", "groups")
 
 
 def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
@@ -342,9 +370,11 @@ def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
     o_ws = (16 * cap + 255) // 256 * 256
     L.ws_bytes = int(lib.gs_radix_sort_workspace_bytes(cap))  # (>= what any T <= cap needs)
     L.o_live = o_ws + (L.ws_bytes + 255) // 256 * 256
-    L.p_ws, L.p_live = base + o_ws, base + L.o_live
-    L.live_words = int(lib.gs_blend_live_words(cap, num_tiles))
-    L.o_flags = L.o_live + 8 * cam.cells * L.live_words
+    live_bytes = live_bitmap_bytes(lib, cam.cells, cap, num_tiles)
+    L.p_ws, L.p_live = base + o_ws, (base + L.o_live if live_bytes else None)
+    L.live_words = int(lib.gs_blend_live_words(cap, num_tiles)) if live_bytes else 0
+    L.o_flags = L.o_live + live_bytes
+    L.groups = cell_batch(cam.cells, cap)  # the backward's cells per batch (flags sized for it)
     L.bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
     return L
 
@@ -388,6 +418,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
 
     fr = _Frame()
     fr.slot_live = None
+    fr.groups = cam.groups
     fr.records, fr.rects, fr.vis, fr.order = records, rects, vis, None
     if n > 0:
         ws = torch.empty((lib.gs_radix_sort_workspace_bytes(n),), dtype=torch.uint8, device=dev)
@@ -499,7 +530,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
                                     L.p_ws, L.ws_bytes, C.byref(alt), s), "tile sort")
     # (with gradients to come: the backward's slot flags zeroed in the same kernel)
     ra = N.GsRangeArgs(T, num_tiles, L.p_tk[alt.value], N.ptr(ranges),
-                       L.big.data_ptr() + L.o_flags if need_grad and cam.groups else None, cam.groups)
+                       L.big.data_ptr() + L.o_flags if need_grad else None, L.groups)
     StageTimer.mark("tile_ranges")
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
@@ -515,10 +546,11 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     # (the blend is queued: views for the frame cost no GPU idle time now)
     kv = L.big[:16 * L.cap].view(i32).view(4, L.cap)
     fr.sorted_gauss = kv[2 + alt.value, :T]
-    fr.live_bits = L.big[L.o_live:L.o_live + 8 * cam.cells * L.live_words].view(torch.int64).view(cam.cells,
-                                                                                               L.live_words)
+    fr.live_bits = (L.big[L.o_live:L.o_live + 8 * cam.cells * L.live_words].view(torch.int64)
+                    .view(cam.cells, L.live_words) if L.live_words else None)
     fr.big = L.big
-    fr.slot_live = L.big[L.o_flags:L.o_flags + cam.groups * T] if need_grad and cam.groups else None
+    fr.groups = L.groups
+    fr.slot_live = L.big[L.o_flags:L.o_flags + L.groups * T] if need_grad else None
     fr.pair_offset, fr.ranges = pair_offset, ranges
     fr.pix_acc, fr.pix_state = pix_acc, pix_state
     return image, alpha, depth, means2d, conics, radii, vis, fr
@@ -547,23 +579,36 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_image = g_image.contiguous()
         g_alpha = None if g_alpha is None else g_alpha.contiguous()
         g_depth = None if g_depth is None else g_depth.contiguous()
-        # one partial per (slot, partial group of the tile: gs_partial_groups);
-        # only the groups that replay an entry write theirs and set its flag
-        if cam.groups:
-            pair_grads = torch.empty((fr.T * cam.groups, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
-            slot_live = fr.slot_live  # (zeroed by the forward's gs_tile_ranges)
-            if slot_live is None:
-                slot_live = torch.zeros((fr.T * cam.groups,), dtype=torch.uint8, device=dev)
-        else:
-            # tiles above GS_DENSE_MAX_TILE: the blend backward adds per-Gaussian
-            # sums into [n, 10] with fp32 atomics (gs_partial_groups == 0)
-            pair_grads = torch.zeros((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
+        # one partial per (slot, cell of the batch); only the cells that
+        # replay an entry write theirs and set its flag.  The cells run in
+        # batches of fr.groups (one batch unless the partials would exceed
+        # PARTIAL_BUDGET_BYTES), each summed by gs_gather_partials in order.
+        G, Q = fr.groups, cam.cells
+        pair_grads = torch.empty((fr.T * G, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
+        slot_live = fr.slot_live  # (zeroed by the forward's gs_tile_ranges)
+        if slot_live is None:
+            slot_live = torch.zeros((fr.T * G,), dtype=torch.uint8, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
-                              fr.live_bits.shape[1], N.ptr(pair_grads), N.ptr(slot_live), fr.T)
-        StageTimer.mark("blend_bwd")
-        N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
+                              0 if fr.live_bits is None else fr.live_bits.shape[1], N.ptr(pair_grads),
+                              N.ptr(slot_live), fr.T, 0, G)
+        if G < Q:
+            batch_sums = torch.empty((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
+            ga = N.GsProjectBwdArgs()
+            ga.g.n = n
+            ga.vis, ga.rects, ga.pair_offset = N.ptr(fr.vis), N.ptr(fr.rects), N.ptr(fr.pair_offset)
+            ga.pair_grads, ga.slot_live, ga.grad_sums = N.ptr(pair_grads), N.ptr(slot_live), N.ptr(batch_sums)
+            for b, c0 in enumerate(range(0, Q, G)):
+                ba.cell_begin, ba.cell_count = c0, min(G, Q - c0)
+                ga.partial_groups = ba.cell_count
+                if b:
+                    slot_live.zero_()
+                N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
+                N.check(lib.gs_gather_partials(C.byref(ga), 1 if b else 0, s), "gs_gather_partials")
+        else:
+            StageTimer.mark("blend_bwd")
+            N.check(lib.gs_blend_backward(C.byref(ba), s), "gs_blend_backward")
     raw = cov3d is None
     out = dict(out or {})
     rows_ready = out.pop("_rows_ready", None)
@@ -582,14 +627,16 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     gc = None if g_conics is None else g_conics.contiguous()
     d_sh = buf("sh_rest", (n, N.GS_SH_REST, 3)) if sh_degree > 0 else None
     gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
-    grad_sums = None if pair_grads is None else (
-        pair_grads if not cam.groups else torch.empty((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev))
+    if pair_grads is not None and fr.groups < cam.cells:
+        grad_sums, pair_grads, slot_live = batch_sums, None, None  # (summed batch by batch above)
+    else:
+        grad_sums = None if pair_grads is None else torch.empty((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
     pb = N.GsProjectBwdArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(fr.vis), N.ptr(fr.rects),
                             # Gaussian order (order=NULL): inputs/outputs stream; walking in depth
                             # order coalesces the slot reads but scatters 10 arrays (measured 2.4x slower)
                             N.ptr(fr.pair_offset), None, N.ptr(pair_grads), N.ptr(gm), N.ptr(gc), N.ptr(d_xyz),
                             N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col), N.ptr(d_op), N.ptr(d_sh),
-                            N.ptr(slot_live), N.ptr(grad_sums))
+                            N.ptr(slot_live), N.ptr(grad_sums), fr.groups)
     StageTimer.mark("project_bwd")
     bounds = [n * k // chunks for k in range(chunks + 1)]
     for lo, hi in zip(bounds[:-1], bounds[1:]):

@@ -32,6 +32,16 @@ production call shape -- a grouped ncclAllReduce of two slices at non-zero
 offsets with ncclAvg on the collective stream behind an event -- on
 rank-dependent integer-valued data, checks the mean on every rank, and checks
 ncclCommCount / ncclCommUserRank against the process group.
+
+Limitation: ncclCommInitRank (step 3) blocks until every rank has joined the
+communicator's bootstrap.  The agreement after step 2 means every rank enters
+it, but a rank that fails inside it before joining (e.g. a device error on
+that rank alone) leaves the others blocked in the call, where no agreement
+can reach them; only the self-check (step 4) is bounded in time.  A
+non-blocking init (ncclCommInitRankConfig with blocking = 0, then polling
+ncclCommGetAsyncError) would bound it too, but would also make every later
+call on the communicator asynchronous (ncclInProgress), a mode this module's
+call sequence was never run in on more than one GPU; it is not used.
 """
 from __future__ import annotations
 

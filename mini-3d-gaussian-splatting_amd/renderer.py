@@ -70,8 +70,9 @@ def effective_tile(tile_size: int, width: int, height: int) -> int:
     if t > max(int(width), int(height)):
         t = max(int(width), int(height), 1)
     if t > N.GS_MAX_TILE:
-        raise ValueError(f"tile_size {tile_size} on a {width}x{height} image: tiles above {N.GS_MAX_TILE} px "
-                         f"that do not cover the image are not supported")
+        raise ValueError(f"tile_size {tile_size} on a {width}x{height} image: a tile edge of {t} px (the "
+                         f"smaller of tile_size and max(W, H)) is above GS_MAX_TILE = {N.GS_MAX_TILE}, "
+                         f"which is not supported")
     return t
 
 

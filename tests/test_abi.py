@@ -109,5 +109,6 @@ def test_workspace_queries(pkg):
     # 8x8 cells per tile: ceil(L/8)^2 (the liveness bitmap and partial layouts)
     assert [lib.gs_tile_quads(t) for t in (1, 8, 9, 12, 16, 24, 32, 256, 0, 257, 4096, 4097)] == \
         [1, 1, 4, 4, 4, 9, 16, 1024, 0, 1089, 262144, 0]
-    # partials per entry: one per cell up to GS_DENSE_MAX_TILE, 0 above (per-Gaussian atomic sums)
-    assert [lib.gs_partial_groups(t) for t in (1, 16, 256, 257, 4096, 0, 4097)] == [1, 4, 1024, 0, 0, 0, 0]
+    # partials per entry of a one-batch backward: one per cell at every tile size (large
+    # tiles may replay their cells in batches, rasterizer.cell_batch); 0 out of range
+    assert [lib.gs_partial_groups(t) for t in (1, 16, 256, 257, 4096, 0, 4097)] == [1, 4, 1024, 1089, 262144, 0, 0]

@@ -444,19 +444,43 @@ def test_blend_ranges_clamped_to_entries(pkg, cuda):
     assert lib.gs_blend_forward(C.byref(fa), stream) == 1
 
 
-def test_deterministic(pkg, cuda):
-    """No float atomics anywhere: two runs are bit-identical, grads included."""
+@pytest.mark.parametrize("tile", [16, 300, 480])
+def test_deterministic(pkg, cuda, tile):
+    """No float atomics anywhere, at any tile size: two runs are
+    bit-identical, grads included.  Tiles of 300 / 480 px (1,444 / 3,600
+    cells) also run with a partial budget that forces cell batches (summed
+    batch by batch by gs_gather_partials) and with no liveness bitmap."""
+    RZ = pkg.rasterizer
     syn = pkg.synthetic
-    sc = syn.make_scene(50000, 480, 270, seed=5, sigma_range=(0.002, 0.02))
-    res = []
-    for _ in range(2):
-        m = syn.to_model(sc, pkg.GaussianModel, cuda)
-        out = pkg.GaussianRenderer().render(Cam(480, 270, sc.fovx, sc.fovy), m,
-                                            pkg.RenderSettings(270, 480, torch.zeros(3)))
-        out["image"].sum().backward()
-        res.append((out["image"].clone(), m._xyz.grad.clone(), m._rotation.grad.clone()))
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
+    sc = syn.make_scene(50000 if tile == 16 else 8000, 480, 270, seed=5, sigma_range=(0.002, 0.02))
+    budgets = [(RZ.PARTIAL_BUDGET_BYTES, RZ.LIVE_BUDGET_BYTES)]
+    if tile > 16:
+        budgets += [(41 * 9000 * 100, RZ.LIVE_BUDGET_BYTES), (41 * 9000 * 300, 1)]
+    saved = budgets[0]
+    outs = []
+    try:
+        for pb, lb in budgets:
+            RZ.PARTIAL_BUDGET_BYTES, RZ.LIVE_BUDGET_BYTES = pb, lb
+            res = []
+            for _ in range(2):
+                m = syn.to_model(sc, pkg.GaussianModel, cuda)
+                out = pkg.GaussianRenderer(tile_size=tile).render(Cam(480, 270, sc.fovx, sc.fovy), m,
+                                                                  pkg.RenderSettings(270, 480, torch.zeros(3)))
+                (out["image"].sum() + out["depth"].mean()).backward()
+                res.append((out["image"].clone(), m._xyz.grad.clone(), m._rotation.grad.clone(),
+                            m._opacity.grad.clone()))
+            for a, b in zip(*res):
+                assert torch.equal(a, b)
+            outs.append(res[0])
+    finally:
+        RZ.PARTIAL_BUDGET_BYTES, RZ.LIVE_BUDGET_BYTES = saved
+    # batched / bitmap-free runs: the same image; gradients summed in another
+    # order (per batch), so equal to rounding
+    for r in outs[1:]:
+        assert torch.equal(r[0], outs[0][0])
+        for a, b in zip(r[1:], outs[0][1:]):
+            scale = float(b.abs().max()) + 1e-12
+            assert float((a - b).abs().max()) <= 1e-5 * scale
 
 
 def test_emit_capacity_guess(pkg, cuda):
@@ -709,9 +733,7 @@ def test_tile_sizes_vs_oracle(pkg, cuda, tile):
 
 @pytest.mark.parametrize("tile", [300, 480, 5000])
 def test_large_tiles_vs_oracle(pkg, cuda, tile):
-    """Tile edges above GS_DENSE_MAX_TILE (256): the blend backward sums each
-    Gaussian's gradient with fp32 atomics (gs_partial_groups == 0, no
-    [T, (L/8)^2] partial buffer).  300: 3 x 2 tiles of 1,444 cells, partial
+    """Large tile edges: 300 -- 3 x 2 tiles of 1,444 cells, partial
     edge tiles; 480: tiles as tall as the image; 5000, far above the image:
     rendered as one tile of max(W, H) = 640 px (renderer.effective_tile), while
     the oracle bins with the edge as given -- the same outputs, as the

@@ -51,8 +51,8 @@ def test_renderer_constructor_range(pkg):
     any tile edge >= 1 (the reference takes any int; 0 divides by zero there)
     and finite radii are taken as given.  The kernels' edge is the tile_size,
     or max(W, H) when it is larger (one tile holds the image either way:
-    effective_tile); above 256 the backward sums per Gaussian
-    (gs_partial_groups == 0)."""
+    effective_tile); tiles of many cells replay them in batches within a
+    memory budget (rasterizer.cell_batch)."""
     for t in (1, 8, 12, 16, 32, 256, 257, 1000, 10 ** 6):
         r = pkg.GaussianRenderer(tile_size=t, radius_max=80.0)
         assert r.tile_size == t and r.radius_max == 80.0
@@ -64,16 +64,39 @@ def test_renderer_constructor_range(pkg):
         c = pkg.camera_params(_Cam(), pkg.RenderSettings(20, 30, torch.zeros(3)), tile_size=t)
         assert (c.tile_size, c.tiles_x, c.tiles_y) == (30, 1, 1)
     big = pkg.RenderSettings(4000, 4000, torch.zeros(3))
-    assert pkg.camera_params(_Cam(), big, tile_size=300).groups == 0  # atomic sums above 256
+    assert pkg.camera_params(_Cam(), big, tile_size=300).groups == 1444  # one partial per 8x8 cell
     assert pkg.camera_params(_Cam(), big, tile_size=256).groups == 1024
-    assert pkg.camera_params(_Cam(), pkg.RenderSettings(5000, 5000, torch.zeros(3)), tile_size=10 ** 6).tile_size == 5000 \
-        if 5000 <= pkg._native.GS_MAX_TILE else True
+    # an image wider than GS_MAX_TILE (4096) cannot be one tile: a tile edge that
+    # would cover it raises (README / INTEGRATION.md "Limits"), where the
+    # reference renders it as one tile
+    assert pkg._native.GS_MAX_TILE == 4096
+    with pytest.raises(ValueError):
+        pkg.camera_params(_Cam(), pkg.RenderSettings(5000, 5000, torch.zeros(3)), tile_size=10 ** 6)
     with pytest.raises(ValueError):  # a 5000-px image in tiles above 4096 px that do not cover it
         pkg.camera_params(_Cam(), pkg.RenderSettings(5000, 5000, torch.zeros(3)), tile_size=4500)
     for bad in (dict(tile_size=0), dict(tile_size=-3), dict(tile_size=8.5), dict(radius_max=float("inf")),
                 dict(radius_min=3.0, radius_max=2.0)):
         with pytest.raises(ValueError):
             pkg.GaussianRenderer(**bad)
+
+
+def test_cell_batches_and_bitmap_budget(pkg):
+    """Bounded memory at any tile size: the backward's partials
+    [T, G] and the forward's liveness bitmap stay within their budgets; the
+    default tile's four cells never batch (the performance path), whatever T."""
+    RZ = pkg.rasterizer
+    lib = pkg._native.load()
+    B = RZ.PARTIAL_BUDGET_BYTES
+    assert RZ.cell_batch(4, 10 ** 9) == 4
+    assert RZ.cell_batch(16, 10 ** 5) == 16
+    for cells, T in ((1444, 1_050_000), (57_600, 1_000_000), (262_144, 4_000_000), (1024, 50_000_000)):
+        g = RZ.cell_batch(cells, T)
+        assert 1 <= g <= cells and (g == 1 or 41 * T * g <= B)
+    # ADVICE r04's case: 1080p, one 1920-px tile (57,600 cells), 1M entries: ~7 GB of bitmap -> none
+    assert RZ.live_bitmap_bytes(lib, 57_600, 1_000_000, 1) == 0
+    assert RZ.live_bitmap_bytes(lib, 4, 4_411_397, 8160) == 8 * 4 * (4_411_397 // 64 + 8160 + 2)
+    small = RZ.live_bitmap_bytes(lib, 1444, 3000, 6)
+    assert 0 < small <= RZ.LIVE_BUDGET_BYTES
 
 
 def test_gaussian_model_layout(pkg):
