@@ -116,6 +116,16 @@ def cell_batch(cells: int, entries: int) -> int:
     return max(1, min(cells, PARTIAL_BUDGET_BYTES // per))
 
 
+def flag_bytes(cells: int, cap: int) -> int:
+    """Slot-flag bytes that hold [T, cell_batch(cells, T)] for every T <= cap
+    (the batch is chosen from the frame's own T, so that the summation order,
+    and with it every gradient bit, depends on the frame only -- not on the
+    capacity guess of the frame before)."""
+    if cells <= _ALWAYS_ONE_BATCH:
+        return cells * cap
+    return max(min(cells * cap, PARTIAL_BUDGET_BYTES // 41), cap)
+
+
 def live_bitmap_bytes(lib, cells: int, entries: int, num_tiles: int) -> int:
     """Bytes of the forward's liveness bitmap, or 0 when it exceeds
     LIVE_BUDGET_BYTES (then none is written; ADVICE r04: at 1080p a tile of
@@ -348,7 +358,7 @@ def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cam: CameraParams, dev):
     nbytes = (16 * cap + 255) // 256 * 256
     nbytes += (int(lib.gs_radix_sort_workspace_bytes(cap)) + 255) // 256 * 256
     nbytes += live_bitmap_bytes(lib, cam.cells, cap, num_tiles)
-    nbytes += (cell_batch(cam.cells, cap) * cap + 255) // 256 * 256  # slot flags (zeroed by gs_tile_ranges)
+    nbytes += (flag_bytes(cam.cells, cap) + 255) // 256 * 256  # slot flags (zeroed by gs_tile_ranges)
     return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
 
 
@@ -374,7 +384,7 @@ def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
     L.p_ws, L.p_live = base + o_ws, (base + L.o_live if live_bytes else None)
     L.live_words = int(lib.gs_blend_live_words(cap, num_tiles)) if live_bytes else 0
     L.o_flags = L.o_live + live_bytes
-    L.groups = cell_batch(cam.cells, cap)  # the backward's cells per batch (flags sized for it)
+    L.groups = 0  # the backward's cells per batch: cell_batch(cells, T), set once T is known
     L.bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
     return L
 
@@ -524,6 +534,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         StageTimer.mark("bin_emit")
         N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
     L = layout
+    L.groups = cell_batch(cam.cells, T)  # (from T alone: the gradients' summation order)
+    assert L.groups * T <= flag_bytes(cam.cells, L.cap)
     alt = C.c_int32(0)
     StageTimer.mark("tile_sort")
     N.check(lib.gs_radix_sort_pairs(L.p_tk[0], L.p_tv[0], L.p_tk[1], L.p_tv[1], T, 0, L.bits, 0,
