@@ -61,9 +61,15 @@ class CameraParams:
     @property
     def groups(self) -> int:
         """Gradient partials a one-batch blend backward writes per list entry
-        (gs_partial_groups): one per cell, 4 at the default tile.  Large tiles
-        may replay their cells in batches (cell_batch)."""
+        (gs_partial_groups): 1 at the default tile (its four cells combined
+        on chip), else one per cell.  Tiles of many cells may replay them in
+        batches (frame_groups)."""
         return _partial_groups(self.tile_size)
+
+    def frame_groups(self, entries: int) -> int:
+        """Partials per entry of one backward batch for a frame of `entries`
+        list entries: the combined default tile's one, else cell_batch."""
+        return self.groups if self.groups < self.cells else cell_batch(self.cells, entries)
 
     def to_struct(self) -> N.GsCamera:
         c = N.GsCamera()
@@ -116,11 +122,13 @@ def cell_batch(cells: int, entries: int) -> int:
     return max(1, min(cells, PARTIAL_BUDGET_BYTES // per))
 
 
-def flag_bytes(cells: int, cap: int) -> int:
-    """Slot-flag bytes that hold [T, cell_batch(cells, T)] for every T <= cap
-    (the batch is chosen from the frame's own T, so that the summation order,
-    and with it every gradient bit, depends on the frame only -- not on the
-    capacity guess of the frame before)."""
+def flag_bytes(cells: int, cap: int, groups: int = 0) -> int:
+    """Slot-flag bytes that hold [T, frame_groups(T)] for every T <= cap (the
+    batch is chosen from the frame's own T, so that the summation order, and
+    with it every gradient bit, depends on the frame only -- not on the
+    capacity guess of the frame before).  groups: gs_partial_groups."""
+    if 0 < groups < cells:
+        return groups * cap  # (combined cells: one batch)
     if cells <= _ALWAYS_ONE_BATCH:
         return cells * cap
     return max(min(cells * cap, PARTIAL_BUDGET_BYTES // 41), cap)
@@ -358,7 +366,7 @@ def _alloc_tile_buffers(lib, cap: int, num_tiles: int, cam: CameraParams, dev):
     nbytes = (16 * cap + 255) // 256 * 256
     nbytes += (int(lib.gs_radix_sort_workspace_bytes(cap)) + 255) // 256 * 256
     nbytes += live_bitmap_bytes(lib, cam.cells, cap, num_tiles)
-    nbytes += (flag_bytes(cam.cells, cap) + 255) // 256 * 256  # slot flags (zeroed by gs_tile_ranges)
+    nbytes += (flag_bytes(cam.cells, cap, cam.groups) + 255) // 256 * 256  # slot flags (zeroed by gs_tile_ranges)
     return torch.empty((nbytes,), dtype=torch.uint8, device=dev), cap
 
 
@@ -384,7 +392,7 @@ def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
     L.p_ws, L.p_live = base + o_ws, (base + L.o_live if live_bytes else None)
     L.live_words = int(lib.gs_blend_live_words(cap, num_tiles)) if live_bytes else 0
     L.o_flags = L.o_live + live_bytes
-    L.groups = 0  # the backward's cells per batch: cell_batch(cells, T), set once T is known
+    L.groups = 0  # the backward's partials per entry and batch: frame_groups(T), set once T is known
     L.bits = max(1, int(math.ceil(math.log2(num_tiles))) if num_tiles > 1 else 1)
     return L
 
@@ -534,8 +542,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         StageTimer.mark("bin_emit")
         N.check(lib.gs_bin_emit(C.byref(ba), s), "gs_bin_emit")
     L = layout
-    L.groups = cell_batch(cam.cells, T)  # (from T alone: the gradients' summation order)
-    assert L.groups * T <= flag_bytes(cam.cells, L.cap)
+    L.groups = cam.frame_groups(T)  # (from T alone: the gradients' summation order)
+    assert L.groups * T <= flag_bytes(cam.cells, L.cap, cam.groups)
     alt = C.c_int32(0)
     StageTimer.mark("tile_sort")
     N.check(lib.gs_radix_sort_pairs(L.p_tk[0], L.p_tv[0], L.p_tk[1], L.p_tv[1], T, 0, L.bits, 0,
@@ -591,9 +599,10 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_image = g_image.contiguous()
         g_alpha = None if g_alpha is None else g_alpha.contiguous()
         g_depth = None if g_depth is None else g_depth.contiguous()
-        # one partial per (slot, cell of the batch); only the cells that
-        # replay an entry write theirs and set its flag.  The cells run in
-        # batches of fr.groups (one batch unless the partials would exceed
+        # one partial per (slot, cell of the batch) -- per slot at the default
+        # tile, whose cells are combined on chip; only replayed entries write
+        # theirs and set its flag.  Other tiles' cells run in batches of
+        # fr.groups (one batch unless the partials would exceed
         # PARTIAL_BUDGET_BYTES), each summed by gs_gather_partials in order.
         G, Q = fr.groups, cam.cells
         pair_grads = torch.empty((fr.T * G, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
@@ -604,8 +613,8 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
                               N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
                               N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
                               0 if fr.live_bits is None else fr.live_bits.shape[1], N.ptr(pair_grads),
-                              N.ptr(slot_live), fr.T, 0, G)
-        if G < Q:
+                              N.ptr(slot_live), fr.T, 0, 0)
+        if G < cam.groups:
             batch_sums = torch.empty((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)
             ga = N.GsProjectBwdArgs()
             ga.g.n = n
@@ -639,7 +648,7 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     gc = None if g_conics is None else g_conics.contiguous()
     d_sh = buf("sh_rest", (n, N.GS_SH_REST, 3)) if sh_degree > 0 else None
     gst = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
-    if pair_grads is not None and fr.groups < cam.cells:
+    if pair_grads is not None and fr.groups < cam.groups:
         grad_sums, pair_grads, slot_live = batch_sums, None, None  # (summed batch by batch above)
     else:
         grad_sums = None if pair_grads is None else torch.empty((n, N.GS_PAIR_GRAD_FLOATS), dtype=f32, device=dev)

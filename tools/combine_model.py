@@ -145,5 +145,98 @@ def ring_partials(n, ls, fins, R):
     return int(combined.sum() + cnt[live & ~combined].sum())
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 2:
     main(sys.argv[1])
+
+
+def chunks_of(pos, a=1.0, b=4.0, word=0.5):
+    """(chunk index per live entry, chunk costs) of one cell wave."""
+    if len(pos) == 0:
+        return np.zeros(0, np.int64), np.zeros(0)
+    w = pos // 64
+    cid = np.empty(len(pos), np.int64)
+    costs = []
+    i, lastw = 0, -1
+    while i < len(pos):
+        c = 0.0
+        if w[i] != lastw:
+            c += word
+            lastw = w[i]
+        j = i
+        while j < len(pos) and j - i < 8 and w[j] == w[i]:
+            j += 1
+        cid[i:j] = len(costs)
+        costs.append(c + a * (j - i) + b)
+        i = j
+    return cid, np.array(costs)
+
+
+def ring_wait(n, ls, R, iters=60):
+    """4 cell waves of one workgroup, ring of R slots, waiting (no spills):
+    an entry live in >= 2 cells occupies slot e mod R from its first
+    deposit until its last; a deposit into a slot still held by an older
+    entry waits for that entry's last deposit; a chunk ends when its last
+    entry's deposit is done.  Returns (workgroup time, own times)."""
+    cnt = np.zeros(n, np.int64)
+    for l in ls:
+        cnt[l] += 1
+    ring = cnt >= 2
+    # previous ring occupant of each entry's slot
+    prev = np.full(n, -1, np.int64)
+    lastocc = {}
+    for e in np.nonzero(ring)[0]:
+        prev[e] = lastocc.get(e % R, -1)
+        lastocc[e % R] = e
+    cc = [chunks_of(l) for l in ls]
+    own = [float(c.sum()) if len(c) else 0.0 for _, c in cc]
+    rel = np.zeros(n)  # release time of each ring entry
+    dep = [np.zeros(len(l)) for l in ls]
+    for _ in range(iters):
+        new_rel = np.zeros(n)
+        for q, l in enumerate(ls):
+            cid, costs = cc[q]
+            if len(l) == 0:
+                continue
+            need = np.where(ring[l] & (prev[l] >= 0), rel[np.maximum(prev[l], 0)], 0.0)
+            t = 0.0
+            d = dep[q]
+            k0 = 0
+            for k in range(len(costs)):
+                k1 = k0
+                while k1 < len(cid) and cid[k1] == k:
+                    k1 += 1
+                r = t + costs[k]
+                dk = np.maximum(r, need[k0:k1])
+                d[k0:k1] = dk
+                t = float(dk.max())
+                k0 = k1
+            np.maximum.at(new_rel, l, d)
+        if np.array_equal(new_rel, rel):
+            break
+        rel = new_rel
+    ends = [float(d.max()) if len(d) else 0.0 for d in dep]
+    return max(ends), own, ends
+
+
+def wait_report(path, Rs=(8, 16, 24, 32, 64)):
+    d = np.load(path)
+    tl = cell_lists(d)
+    rng = np.random.default_rng(0)
+    sample = rng.choice(len(tl), size=min(1500, len(tl)), replace=False)
+    for R in Rs:
+        wg = own_sum = end_sum = maxown = 0.0
+        for t in sample:
+            n, ls = tl[t]
+            if n == 0:
+                continue
+            m, own, ends = ring_wait(n, ls, R)
+            wg += m
+            own_sum += sum(own)
+            end_sum += sum(ends)
+            maxown += max(own)
+        print(f"wait R={R:3d}: waves' end / own work {end_sum / own_sum:.3f}; workgroup (slowest wave) "
+              f"{wg / maxown:.3f} x the slowest wave's own work; 4 x workgroup / own work {4 * wg / own_sum:.3f}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "wait":
+    wait_report(sys.argv[1])
