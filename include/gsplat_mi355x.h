@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 17
+#define GS_ABI_VERSION 18
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 4096      /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
                                  of at least max(W, H) renders the same as any larger one (one tile
@@ -54,7 +54,10 @@ typedef enum gs_status {
   GS_OK = 0,
   GS_ERR_INVALID_ARG = 1,
   GS_ERR_LAUNCH = 2,
-  GS_ERR_UNSUPPORTED = 3
+  GS_ERR_UNSUPPORTED = 3,
+  /* gs_render_forward only -- not errors, what the caller does next: */
+  GS_NEED_CAPACITY = 4,   /* T list entries exceed the tile workspace: grow it and call again with resume = 1 */
+  GS_RETRY_FULL_KEYS = 5  /* a visible depth left the depth-key window: render again with key_bits = 32 */
 } gs_status;
 
 typedef void *gs_stream_t; /* hipStream_t */
@@ -454,6 +457,80 @@ typedef struct gs_densify_args {
 size_t gs_densify_workspace_bytes(int32_t n);
 gs_status gs_densify_count(const gs_densify_args *a, gs_stream_t stream);
 gs_status gs_densify_emit(const gs_densify_args *a, gs_stream_t stream);
+
+/* ---- Frame entry points: the stages above in one call per direction -------
+ * gs_render_forward runs what GaussianRenderer.render does (renderer.py:31-114)
+ * -- projection + culling, depth sort, binning, tile sort, ranges, blend --
+ * and gs_render_backward its autograd backward, over two caller-owned
+ * workspaces the library lays out: a frame workspace (per Gaussian and per
+ * pixel, gs_frame_workspace_bytes) and a tile workspace (per list entry, for up
+ * to `capacity` entries, gs_tile_workspace_bytes).  The host reads the
+ * frame's counts (M, T, the visible depth range) back once, inside
+ * gs_render_forward, by polling a pinned buffer the count writes through its
+ * device address.  Both workspaces must stay untouched from the forward to
+ * its backward. */
+typedef struct gs_frame_buffers {
+  void *frame_ws;        /* gs_frame_workspace_bytes(n, W, H, tile_size) */
+  size_t frame_ws_bytes;
+  void *tile_ws;         /* gs_tile_workspace_bytes(capacity, tiles, live_cells, flag_groups) */
+  size_t tile_ws_bytes;
+  int64_t capacity;      /* list entries the tile workspace holds */
+  int32_t live_cells;    /* cells of the liveness bitmap (gs_tile_quads), or 0: none (a memory budget) */
+  int32_t flag_groups;   /* slot flags per entry: the backward's partial groups per batch */
+} gs_frame_buffers;
+size_t gs_frame_workspace_bytes(int32_t n, int32_t width, int32_t height, int32_t tile_size);
+size_t gs_tile_workspace_bytes(int64_t capacity, int32_t num_tiles, int32_t live_cells, int32_t flag_groups);
+
+typedef struct gs_render_fwd_args {
+  gs_camera cam;
+  gs_gaussians g;
+  float *means2d, *conics, *radii; /* outputs, as gs_project_args */
+  uint8_t *vis;
+  float *image, *alpha, *depth;    /* outputs, as gs_blend_fwd_args */
+  gs_frame_buffers fb;
+  uint32_t key_base;               /* the depth-key window (gs_project_args) */
+  int32_t key_bits;
+  int32_t depth_sort_msd;          /* 1: gs_depth_sort_msd for windows of 9..31 bits */
+  int32_t zero_slot_flags;         /* a backward follows: clear its slot flags [T, flag_groups] */
+  uint32_t *host_counters_dev;     /* pinned [8] u32: device address (gs_bin_args.host_counters) */
+  volatile uint32_t *host_counters_host; /* ... and host address of the same buffer */
+  uint32_t host_seq;               /* this frame's sequence word (never the previous frame's) */
+  uint32_t *pair_counts;           /* optional, gs_blend_fwd_args.pair_counts */
+  int32_t resume;                  /* 1: continue after GS_NEED_CAPACITY, with a tile workspace of >= T */
+  /* results (and state for resume / the backward) */
+  int32_t M, T;
+  uint32_t depth_min_bits, depth_max_bits; /* counters[2..3] */
+  int32_t depth_alt, tile_alt;
+} gs_render_fwd_args;
+/* GS_OK; M == 0: nothing drawn (renderer.py:74-83's background image is the
+ * caller's); GS_NEED_CAPACITY / GS_RETRY_FULL_KEYS: see gs_status. */
+gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream);
+
+typedef struct gs_render_bwd_args {
+  gs_camera cam;
+  gs_gaussians g;
+  gs_frame_buffers fb;             /* the forward's */
+  int32_t M, T, tile_alt;          /* the forward's results */
+  const float *means2d, *conics;   /* the forward's outputs */
+  const uint8_t *vis;
+  const float *g_image, *g_alpha, *g_depth; /* pixel cotangents (g_image NULL: none) */
+  const float *g_means2d, *g_conics;        /* optional */
+  float *pair_grads;               /* [T * fb.flag_groups, GS_PARTIAL_STRIDE] scratch */
+  int32_t flags_zeroed;            /* the forward cleared the slot flags (zero_slot_flags) */
+  int32_t project;                 /* 1: also run gs_project_backward over every Gaussian */
+  float *d_xyz, *d_cov3d, *d_scaling, *d_rotation, *d_color_logits, *d_opacity, *d_sh_rest; /* as gs_project_bwd_args */
+  float *grad_sums;                /* result: [n, 10] gathered sums in the frame workspace (for a
+                                      caller's own gs_project_backward, e.g. per row range) */
+} gs_render_bwd_args;
+gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream);
+/* Byte offsets of the buffers inside the two workspaces (for diagnostics and
+ * tests that inspect a frame): frame -- records, rects, depth keys [2,n],
+ * depth ids [2,n], key_minmax, counters, sort workspace, binning workspace,
+ * pair_offset, tile ranges, pix_acc, pix_state, grad_sums, total; tile -- tile
+ * keys (two halves), Gaussian ids (two halves), sort workspace, liveness
+ * bitmap, slot flags, total, liveness words per cell. */
+void gs_frame_offsets(int32_t n, int32_t width, int32_t height, int32_t tile_size, size_t out[14]);
+void gs_tile_offsets(int64_t capacity, int32_t num_tiles, int32_t live_cells, int32_t flag_groups, size_t out[9]);
 
 /* ---- misc --------------------------------------------------------------- */
 int32_t gs_abi_version(void);

@@ -27,7 +27,8 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 17
+GS_ABI_VERSION = 18
+GS_NEED_CAPACITY, GS_RETRY_FULL_KEYS = 4, 5  # gs_render_forward: what to do next (not errors)
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
 _vp = C.c_void_p
@@ -105,6 +106,35 @@ class GsProjectBwdArgs(C.Structure):
     ]
 
 
+class GsFrameBuffers(C.Structure):
+    _fields_ = [
+        ("frame_ws", _vp), ("frame_ws_bytes", C.c_size_t), ("tile_ws", _vp), ("tile_ws_bytes", C.c_size_t),
+        ("capacity", C.c_int64), ("live_cells", C.c_int32), ("flag_groups", C.c_int32),
+    ]
+
+
+class GsRenderFwdArgs(C.Structure):
+    _fields_ = [
+        ("cam", GsCamera), ("g", GsGaussians), ("means2d", _vp), ("conics", _vp), ("radii", _vp), ("vis", _vp),
+        ("image", _vp), ("alpha", _vp), ("depth", _vp), ("fb", GsFrameBuffers), ("key_base", C.c_uint32),
+        ("key_bits", C.c_int32), ("depth_sort_msd", C.c_int32), ("zero_slot_flags", C.c_int32),
+        ("host_counters_dev", _vp), ("host_counters_host", _vp), ("host_seq", C.c_uint32), ("pair_counts", _vp),
+        ("resume", C.c_int32), ("M", C.c_int32), ("T", C.c_int32), ("depth_min_bits", C.c_uint32),
+        ("depth_max_bits", C.c_uint32), ("depth_alt", C.c_int32), ("tile_alt", C.c_int32),
+    ]
+
+
+class GsRenderBwdArgs(C.Structure):
+    _fields_ = [
+        ("cam", GsCamera), ("g", GsGaussians), ("fb", GsFrameBuffers), ("M", C.c_int32), ("T", C.c_int32),
+        ("tile_alt", C.c_int32), ("means2d", _vp), ("conics", _vp), ("vis", _vp), ("g_image", _vp),
+        ("g_alpha", _vp), ("g_depth", _vp), ("g_means2d", _vp), ("g_conics", _vp), ("pair_grads", _vp),
+        ("flags_zeroed", C.c_int32), ("project", C.c_int32), ("d_xyz", _vp), ("d_cov3d", _vp),
+        ("d_scaling", _vp), ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
+        ("grad_sums", _vp),
+    ]
+
+
 GS_ADAM_MAX_TENSORS = 8
 
 
@@ -159,7 +189,8 @@ EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
     "gs_tile_ranges", "gs_blend_live_words", "gs_tile_quads", "gs_partial_groups", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-    "gs_gather_partials", "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
+    "gs_gather_partials", "gs_frame_workspace_bytes", "gs_tile_workspace_bytes", "gs_render_forward",
+    "gs_render_backward", "gs_frame_offsets", "gs_tile_offsets", "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
     "gs_densify_workspace_bytes", "gs_densify_count", "gs_densify_emit",
 )
 
@@ -197,6 +228,16 @@ def _declare(lib):
     lib.gs_blend_backward.argtypes = [P(GsBlendBwdArgs), _vp]
     lib.gs_project_backward.argtypes = [P(GsProjectBwdArgs), _vp]
     lib.gs_gather_partials.argtypes = [P(GsProjectBwdArgs), C.c_int32, _vp]
+    lib.gs_frame_workspace_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32]
+    lib.gs_frame_workspace_bytes.restype = C.c_size_t
+    lib.gs_tile_workspace_bytes.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
+    lib.gs_tile_workspace_bytes.restype = C.c_size_t
+    lib.gs_render_forward.argtypes = [P(GsRenderFwdArgs), _vp]
+    lib.gs_render_backward.argtypes = [P(GsRenderBwdArgs), _vp]
+    lib.gs_frame_offsets.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, P(C.c_size_t)]
+    lib.gs_frame_offsets.restype = None
+    lib.gs_tile_offsets.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32, P(C.c_size_t)]
+    lib.gs_tile_offsets.restype = None
     lib.gs_adam_step.argtypes = [P(GsAdamArgs), _vp]
     lib.gs_loss_workspace_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32]
     lib.gs_loss_workspace_bytes.restype = C.c_size_t
@@ -208,7 +249,7 @@ def _declare(lib):
     lib.gs_densify_emit.argtypes = [P(GsDensifyArgs), _vp]
     for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_count", "gs_bin_emit",
               "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-              "gs_gather_partials", "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
+              "gs_gather_partials", "gs_render_forward", "gs_render_backward", "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
         getattr(lib, f).restype = C.c_int
 
 

@@ -13,7 +13,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", n) for n in ("gsplat_mi355x.hip", "gs_loss.hip", "gs_densify.hip")]
+SRC = [os.path.join(HERE, "csrc", n) for n in ("gsplat_mi355x.hip", "gs_loss.hip", "gs_densify.hip", "gs_render.hip")]
 HDR = [os.path.join(ROOT, "include", "gsplat_mi355x.h"), os.path.join(HERE, "csrc", "gs_internal.h")]
 OUT = os.path.join(HERE, "libgsplat_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -397,6 +397,150 @@ def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
     return L
 
 
+# Frames at the default tile run through the library's frame entry points
+# (gs_render_forward / gs_render_backward: one call per direction over two
+# workspaces, ABI 18) unless GS_FRAME_CALLS=0; other tile sizes, and hosts
+# whose pinned counters have no device address, take the stage-by-stage path
+# below.  The two paths launch the same kernels on the same data: their
+# outputs and gradients are bit-identical (test_frame_entry_points_match).
+_FRAME_CALLS = os.environ.get("GS_FRAME_CALLS", "1") != "0"
+_WS_BYTES: dict = {}  # (n, W, H, tile) -> gs_frame_workspace_bytes
+
+
+class _FastFrame:
+    """One forward's state for its backward, in the frame and tile
+    workspaces (gs_render_forward).  The buffers the tests and the bench
+    inspect are views made on demand (gs_frame_offsets / gs_tile_offsets)."""
+    __slots__ = ("fa", "frame_ws", "tile_ws", "M", "T", "groups", "_off", "_toff", "n", "HW", "tiles", "cells",
+                 "slot_live_zeroed", "vis")
+
+    def _o(self):
+        if self._off is None:
+            lib = N.load()
+            fo = (C.c_size_t * 14)()
+            c = self.fa.cam
+            lib.gs_frame_offsets(self.n, c.image_width, c.image_height, c.tile_size, fo)
+            to = (C.c_size_t * 9)()
+            fb = self.fa.fb
+            lib.gs_tile_offsets(fb.capacity, self.tiles, fb.live_cells, fb.flag_groups, to)
+            self._off, self._toff = list(fo), list(to)
+        return self._off, self._toff
+
+    def _f(self, i, nbytes, dtype, shape):
+        o = self._o()[0][i]
+        return self.frame_ws[o:o + nbytes].view(dtype).view(shape)
+
+    def _t(self, i, nbytes, dtype, shape):
+        o = self._o()[1][i]
+        return self.tile_ws[o:o + nbytes].view(dtype).view(shape)
+
+    records = property(lambda s: s._f(0, 4 * N.GS_RECORD_FLOATS * s.n, torch.float32, (s.n, N.GS_RECORD_FLOATS)))
+    rects = property(lambda s: s._f(1, 8 * s.n, torch.int32, (s.n, 2)))
+    order = property(lambda s: s._f(3, 8 * s.n, torch.int32, (2, s.n))[s.fa.depth_alt])
+    pair_offset = property(lambda s: s._f(8, 4 * s.n, torch.int32, (s.n,)))
+    ranges = property(lambda s: s._f(9, 8 * s.tiles, torch.int32, (s.tiles, 2)))
+    pix_acc = property(lambda s: s._f(10, 16 * s.HW, torch.float32, (s.HW, 4)))
+    pix_state = property(lambda s: s._f(11, 8 * s.HW, torch.float32, (s.HW, 2)))
+    sorted_gauss = property(lambda s: s._t(2 + s.fa.tile_alt, 4 * s.T, torch.int32, (s.T,)))
+    live_bits = property(lambda s: s._t(5, 8 * s.cells * s._o()[1][8], torch.int64, (s.cells, s._o()[1][8])))
+    slot_live = property(lambda s: s._t(6, s.groups * s.T, torch.uint8, (s.groups * s.T,)))
+
+
+
+def _host_counters(dev) -> "_HostCounters":
+    per_thread = getattr(_HOST_COUNTERS, "bufs", None)
+    if per_thread is None:
+        per_thread = _HOST_COUNTERS.bufs = {}
+    hc = per_thread.get(dev)
+    if hc is None:
+        hc = per_thread[dev] = _HostCounters()
+    return hc
+
+
+def _forward_frame(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest,
+                   sh_degree, pair_counts, depth_window_ok, need_grad, hc):
+    """forward_pipeline through gs_render_forward (the default tile)."""
+    lib = N.load()
+    dev = xyz.device
+    n = int(xyz.shape[0])
+    H, W = int(cam.image_height), int(cam.image_width)
+    f32 = torch.float32
+    s = _stream()
+    tiles = cam.tiles_x * cam.tiles_y
+    key = (n, W, H, cam.tile_size)
+    fws = _WS_BYTES.get(key)
+    if fws is None:
+        fws = _WS_BYTES[key] = int(lib.gs_frame_workspace_bytes(n, W, H, cam.tile_size))
+    fa = N.GsRenderFwdArgs()
+    fa.cam = cam.to_struct()
+    fa.g = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
+    means2d = torch.empty((n, 2), dtype=f32, device=dev)
+    conics = torch.empty((n, 2, 2), dtype=f32, device=dev)
+    radii = torch.empty((n,), dtype=f32, device=dev)
+    vis = torch.empty((n,), dtype=torch.bool, device=dev)
+    image = torch.empty((3, H, W), dtype=f32, device=dev)
+    alpha = torch.empty((1, H, W), dtype=f32, device=dev)
+    depth = torch.empty((1, H, W), dtype=f32, device=dev)
+    frame_ws = torch.empty((fws,), dtype=torch.uint8, device=dev)
+    fa.means2d, fa.conics, fa.radii, fa.vis = (means2d.data_ptr(), conics.data_ptr(), radii.data_ptr(),
+                                               vis.data_ptr())
+    fa.image, fa.alpha, fa.depth = image.data_ptr(), alpha.data_ptr(), depth.data_ptr()
+    fb = fa.fb
+    fb.frame_ws, fb.frame_ws_bytes = frame_ws.data_ptr(), fws
+    fb.live_cells, fb.flag_groups = cam.cells, cam.groups
+    cap = _T_SEEN.get(dev, 0)
+    cap = cap + cap // 4 + 4096 if cap else 0
+    tile_ws = None
+    if cap:
+        tws = int(lib.gs_tile_workspace_bytes(cap, tiles, cam.cells, cam.groups))
+        tile_ws = torch.empty((tws,), dtype=torch.uint8, device=dev)
+        fb.tile_ws, fb.tile_ws_bytes, fb.capacity = tile_ws.data_ptr(), tws, cap
+    window = _window_for(dev) if depth_window_ok else None
+    fa.key_base, fa.key_bits = window if window is not None else (0, 32)
+    msd = _DEPTH_MSD and window is not None and 9 <= fa.key_bits <= 31
+    backoff = _MSD_BACKOFF.get(dev, 0)
+    if msd and backoff:
+        _MSD_BACKOFF[dev] = backoff - 1
+    fa.depth_sort_msd = 1 if (msd and not backoff) else 0
+    fa.zero_slot_flags = 1 if need_grad else 0
+    hc.seq = hc.seq % 0x7FFFFFFF + 1
+    fa.host_counters_dev, fa.host_counters_host, fa.host_seq = hc.dptr, hc.t.data_ptr(), hc.seq
+    fa.pair_counts = N.ptr(pair_counts)
+    st = lib.gs_render_forward(C.byref(fa), s)
+    if st == N.GS_RETRY_FULL_KEYS:
+        # a visible depth outside the window, or an MSD bucket over capacity
+        if fa.depth_max_bits == _POISON:
+            _MSD_BACKOFF[dev] = _MSD_BACKOFF_FRAMES
+        else:
+            _note_window_miss(dev)
+        _T_SEEN[dev] = fa.T
+        return forward_pipeline(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit,
+                                sh_rest, sh_degree, pair_counts, depth_window_ok=False, need_grad=need_grad)
+    if st == N.GS_NEED_CAPACITY:
+        cap = fa.T
+        tws = int(lib.gs_tile_workspace_bytes(cap, tiles, cam.cells, cam.groups))
+        tile_ws = torch.empty((tws,), dtype=torch.uint8, device=dev)
+        fb.tile_ws, fb.tile_ws_bytes, fb.capacity = tile_ws.data_ptr(), tws, cap
+        fa.resume = 1
+        st = lib.gs_render_forward(C.byref(fa), s)
+    N.check(st, "gs_render_forward")
+    M, T = int(fa.M), int(fa.T)
+    if n > 0:
+        _T_SEEN[dev] = T
+        _record_depths(dev, int(fa.depth_min_bits), int(fa.depth_max_bits))
+    fr = _FastFrame()
+    fr.fa, fr.frame_ws, fr.tile_ws, fr.M, fr.T = fa, frame_ws, tile_ws, M, T
+    fr.groups, fr._off, fr._toff, fr.n, fr.HW, fr.tiles, fr.cells = cam.groups, None, None, n, H * W, tiles, cam.cells
+    fr.slot_live_zeroed = bool(need_grad)
+    fr.vis = vis
+    if M == 0:
+        # renderer.py:74-83: bg once (not doubled, not clamped), zero alpha/depth
+        image = torch.tensor(cam.bg, dtype=f32, device=dev).view(3, 1, 1).repeat(1, H, W)
+        alpha = torch.zeros((1, H, W), dtype=f32, device=dev)
+        depth = torch.zeros((1, H, W), dtype=f32, device=dev)
+    return image, alpha, depth, means2d, conics, radii, vis, fr
+
+
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
                      sh_rest=None, sh_degree=0, pair_counts=None, depth_window_ok=True, need_grad=False):
     """pair_counts: optional int32 [H*W] the blend fills with each pixel's
@@ -407,6 +551,11 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     per 8 bits, gs_project_args.key_base); this frame's range, read back with
     (M, T), says whether the window held -- if not, the frame is rendered
     again with full 32-bit keys (depth_window_ok=False)."""
+    if _FRAME_CALLS and cam.tile_size == N.GS_DEFAULT_TILE:
+        hc = _host_counters(xyz.device)
+        if hc.dptr is not None:
+            return _forward_frame(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest,
+                                  sh_degree, pair_counts, depth_window_ok, need_grad, hc)
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -585,6 +734,9 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     (optional): called with (lo, hi) once the gradient rows of Gaussians
     [lo, hi) are queued, the last stage running in out["_chunks"] ranges so
     that a range's all-reduce overlaps the next range's kernels."""
+    if isinstance(fr, _FastFrame):
+        return _backward_frame(cam, fr, xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics, g_image,
+                               g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit, sh_rest, sh_degree, out)
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -665,6 +817,79 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         N.check(lib.gs_project_backward(C.byref(part), s), "gs_project_backward")
         if rows_ready is not None:
             rows_ready(lo, hi)
+    StageTimer.mark("~end_bwd")
+    return d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh
+
+
+def _backward_frame(cam: CameraParams, fr: _FastFrame, xyz, cov3d, scaling, rotation, logits, opacity, means2d,
+                    conics, g_image, g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit, sh_rest, sh_degree, out):
+    """backward_pipeline through gs_render_backward (the frame of
+    _forward_frame): the blend backward and the gather in the library, then
+    the projection backward -- there too unless the data-parallel reduction
+    wants the rows in ranges."""
+    lib = N.load()
+    dev = xyz.device
+    n = int(xyz.shape[0])
+    f32 = torch.float32
+    s = _stream()
+    pixel_grads = g_image is not None or g_alpha is not None or g_depth is not None
+    ba = N.GsRenderBwdArgs()
+    fa = fr.fa
+    ba.cam, ba.fb, ba.M, ba.T, ba.tile_alt = fa.cam, fa.fb, fr.M, fr.T, fa.tile_alt
+    ba.g = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
+    ba.means2d, ba.conics, ba.vis = means2d.data_ptr(), conics.data_ptr(), fa.vis
+    pair_grads = None
+    if fr.M > 0 and fr.T > 0 and pixel_grads:
+        if g_image is None:
+            g_image = torch.zeros((3, cam.image_height, cam.image_width), dtype=f32, device=dev)
+        g_image = g_image.contiguous()
+        g_alpha = None if g_alpha is None else g_alpha.contiguous()
+        g_depth = None if g_depth is None else g_depth.contiguous()
+        pair_grads = torch.empty((fr.T * fr.groups, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
+        ba.g_image, ba.g_alpha, ba.g_depth = N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth)
+        ba.pair_grads = pair_grads.data_ptr()
+        ba.flags_zeroed = 1 if fr.slot_live_zeroed else 0
+    gm = None if g_means2d is None else g_means2d.contiguous()
+    gc = None if g_conics is None else g_conics.contiguous()
+    ba.g_means2d, ba.g_conics = N.ptr(gm), N.ptr(gc)
+    raw = cov3d is None
+    out = dict(out or {})
+    rows_ready = out.pop("_rows_ready", None)
+    chunks = int(out.pop("_chunks", 1)) if rows_ready is not None else 1
+
+    def buf(name, shape):
+        t = out.get(name)
+        return t.view(shape) if t is not None else torch.empty(shape, dtype=f32, device=dev)
+    d_xyz = buf("xyz", (n, 3))
+    d_cov = None if raw else torch.empty((n, 3, 3), dtype=f32, device=dev)
+    d_scl = buf("scaling", (n, 3)) if raw else None
+    d_rot = buf("rotation", (n, 4)) if raw else None
+    d_col = buf("color", (n, 3))
+    d_op = buf("opacity", (n,))
+    d_sh = buf("sh_rest", (n, N.GS_SH_REST, 3)) if sh_degree > 0 else None
+    ba.d_xyz, ba.d_cov3d, ba.d_scaling, ba.d_rotation = N.ptr(d_xyz), N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot)
+    ba.d_color_logits, ba.d_opacity, ba.d_sh_rest = N.ptr(d_col), N.ptr(d_op), N.ptr(d_sh)
+    ba.project = 1 if chunks == 1 else 0
+    StageTimer.mark("blend_bwd")
+    N.check(lib.gs_render_backward(C.byref(ba), s), "gs_render_backward")
+    if chunks == 1:
+        StageTimer.mark("~end_bwd")
+        if rows_ready is not None:
+            rows_ready(0, n)
+        return d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh
+    # the projection backward per row range, each range's reduction issued
+    # as soon as its rows are queued
+    fo = fr._o()[0]
+    fws = fr.frame_ws.data_ptr()
+    pb = N.GsProjectBwdArgs(fa.cam, ba.g, N.ptr(means2d), N.ptr(conics), fa.vis, fws + fo[1], fws + fo[8], None,
+                            None, N.ptr(gm),
+                            N.ptr(gc), N.ptr(d_xyz), N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col),
+                            N.ptr(d_op), N.ptr(d_sh), None, ba.grad_sums if pair_grads is not None else None, 0)
+    StageTimer.mark("project_bwd")
+    bounds = [n * k // chunks for k in range(chunks + 1)]
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        N.check(lib.gs_project_backward(C.byref(_rows_of(pb, lo, hi)), s), "gs_project_backward")
+        rows_ready(lo, hi)
     StageTimer.mark("~end_bwd")
     return d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh
 

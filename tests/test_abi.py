@@ -15,7 +15,7 @@ HDR = os.path.join(ROOT, "include", "gsplat_mi355x.h")
 
 def declared_functions():
     src = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:gs_status|size_t|int32_t|const char \*)\s*(gs_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:gs_status|size_t|int32_t|void|const char \*)\s*(gs_\w+)\s*\(", src, re.M)))
 
 
 def test_header_and_binding_agree(pkg):
@@ -38,7 +38,8 @@ def test_abi_version(pkg):
 def test_struct_layouts_match_c(pkg, tmp_path):
     N = pkg._native
     names = ["gs_camera", "gs_gaussians", "gs_project_args", "gs_bin_args", "gs_range_args",
-             "gs_blend_fwd_args", "gs_blend_bwd_args", "gs_project_bwd_args", "gs_adam_args", "gs_loss_args", "gs_densify_args"]
+             "gs_blend_fwd_args", "gs_blend_bwd_args", "gs_project_bwd_args", "gs_adam_args", "gs_loss_args", "gs_densify_args",
+             "gs_frame_buffers", "gs_render_fwd_args", "gs_render_bwd_args"]
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "gsplat_mi355x.h"\nint main(){' +
                    "".join('printf("%%zu\\n", sizeof(%s));' % n for n in names) + "}")
@@ -47,7 +48,7 @@ def test_struct_layouts_match_c(pkg, tmp_path):
     sizes = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     py = [C.sizeof(t) for t in (N.GsCamera, N.GsGaussians, N.GsProjectArgs, N.GsBinArgs, N.GsRangeArgs,
                                 N.GsBlendFwdArgs, N.GsBlendBwdArgs, N.GsProjectBwdArgs, N.GsAdamArgs,
-                                N.GsLossArgs, N.GsDensifyArgs)]
+                                N.GsLossArgs, N.GsDensifyArgs, N.GsFrameBuffers, N.GsRenderFwdArgs, N.GsRenderBwdArgs)]
     assert sizes == py
 
 

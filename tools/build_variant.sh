@@ -7,6 +7,6 @@ name=$1; shift
 mkdir -p "$R/ab"
 C=$R/mini-3d-gaussian-splatting_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-slp-vectorize \
-  -Wall -Wno-unused-function -I "$R/include" "$@" "$C/gsplat_mi355x.hip" "$C/gs_loss.hip" "$C/gs_densify.hip" \
+  -Wall -Wno-unused-function -I "$R/include" "$@" "$C/gsplat_mi355x.hip" "$C/gs_loss.hip" "$C/gs_densify.hip" "$C/gs_render.hip" \
   -o "$R/ab/$name.so"
 echo "built ab/$name.so"
