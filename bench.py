@@ -244,9 +244,14 @@ def main():
         dt = float(t.item())
     StageTimer.only = None
     StageTimer.reset()
+    # the per-stage breakdown from the stage-by-stage path (the same kernels;
+    # the frame entry points would time only the blend backward)
+    from mini3dgs_amd import rasterizer as _RZ
+    frame_calls, _RZ._FRAME_CALLS = _RZ._FRAME_CALLS, False
     for _ in range(a.diag_steps):
         step()
         frames = frames[-1:]
+    _RZ._FRAME_CALLS = frame_calls
     stages = {k: sum(v) / len(v) for k, v in StageTimer.durations_ms().items()}
     StageTimer.enabled = False
     ms_per_step = 1000.0 * dt / a.steps
@@ -332,7 +337,9 @@ def main():
                        "parallelism": f"dp{world} (one view per GPU)", "visible": M, "tile_touches": T,
                        "records_consumed": R, "evaluated_pairs": E, "contributing_pairs": Cc},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
-            "stages_note": f"HIP-event intervals from {a.diag_steps} diagnostic steps after the timed region "
+            "stages_note": f"HIP-event intervals from {a.diag_steps} diagnostic steps after the timed region, "
+                           "run stage by stage (GS_FRAME_CALLS=0 path: the same kernels as the timed steps' frame "
+                           "entry points) "
                            "(each interval also holds any host launch gap before its kernels; kernel-only "
                            "times: profiles/*/kernel_stats_*.csv)",
             "roofline": roof,

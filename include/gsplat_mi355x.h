@@ -521,6 +521,8 @@ typedef struct gs_render_bwd_args {
   float *d_xyz, *d_cov3d, *d_scaling, *d_rotation, *d_color_logits, *d_opacity, *d_sh_rest; /* as gs_project_bwd_args */
   float *grad_sums;                /* result: [n, 10] gathered sums in the frame workspace (for a
                                       caller's own gs_project_backward, e.g. per row range) */
+  void *blend_events[2];           /* optional hipEvent_t pair, recorded on the stream right before and
+                                      after the blend backward launch(es): its time alone (profiling) */
 } gs_render_bwd_args;
 gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream);
 /* Byte offsets of the buffers inside the two workspaces (for diagnostics and

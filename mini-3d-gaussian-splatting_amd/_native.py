@@ -131,7 +131,7 @@ class GsRenderBwdArgs(C.Structure):
         ("g_alpha", _vp), ("g_depth", _vp), ("g_means2d", _vp), ("g_conics", _vp), ("pair_grads", _vp),
         ("flags_zeroed", C.c_int32), ("project", C.c_int32), ("d_xyz", _vp), ("d_cov3d", _vp),
         ("d_scaling", _vp), ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
-        ("grad_sums", _vp),
+        ("grad_sums", _vp), ("blend_events", _vp * 2),
     ]
 
 

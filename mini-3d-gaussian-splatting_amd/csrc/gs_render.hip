@@ -308,6 +308,9 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
     ga.pair_grads = a->pair_grads;
     ga.slot_live = flags;
     ga.grad_sums = grad_sums;
+    hipEvent_t ev0 = (hipEvent_t)a->blend_events[0], ev1 = (hipEvent_t)a->blend_events[1];
+    if (ev0 && hipEventRecord(ev0, (hipStream_t)stream) != hipSuccess)
+      return gs_internal_fail(GS_ERR_LAUNCH, "%s: hipEventRecord failed", what);
     const int32_t one = gs_partial_groups(L);
     if (G >= one || G >= cells) {
       // one batch: every cell (or the tile's combined partials)
@@ -317,6 +320,8 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
       if (!a->flags_zeroed && hipMemsetAsync(flags, 0, (size_t)a->T * (size_t)G, (hipStream_t)stream) != hipSuccess)
         return gs_internal_fail(GS_ERR_LAUNCH, "%s: slot flag memset failed", what);
       if ((st = gs_blend_backward(&b, stream))) return st;
+      if (ev1 && hipEventRecord(ev1, (hipStream_t)stream) != hipSuccess)
+        return gs_internal_fail(GS_ERR_LAUNCH, "%s: hipEventRecord failed", what);
       if ((st = gs_gather_partials(&ga, 0, stream))) return st;
     } else {
       // cell batches of G (bounded memory), summed in batch order
@@ -330,6 +335,8 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
         if ((st = gs_blend_backward(&b, stream))) return st;
         if ((st = gs_gather_partials(&ga, bi ? 1 : 0, stream))) return st;
       }
+      if (ev1 && hipEventRecord(ev1, (hipStream_t)stream) != hipSuccess)  // (batches: gathers included)
+        return gs_internal_fail(GS_ERR_LAUNCH, "%s: hipEventRecord failed", what);
     }
   }
   if (!a->project) return GS_OK;  // (the caller runs gs_project_backward itself, e.g. per row range)

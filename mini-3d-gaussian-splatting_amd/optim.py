@@ -80,14 +80,87 @@ class FusedAdam(torch.optim.Optimizer):
                                             N.ptr(out) + 4 * off if out is not None else None)
                 N.check(lib.gs_adam_step(C.byref(a), stream), "gs_adam_step")
 
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """Optimizer.zero_grad without its profiler annotation (host time
+        the small configurations are bound by); same semantics."""
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    if set_to_none:
+                        p.grad = None
+                    else:
+                        if p.grad.grad_fn is not None:
+                            p.grad.detach_()
+                        else:
+                            p.grad.requires_grad_(False)
+                        p.grad.zero_()
+
     @torch.no_grad()
     def step(self, closure=None):
+        """One Adam step over every parameter with a gradient.  The launch
+        descriptors are kept between steps and only the per-step fields
+        (gradient address, lr, bias corrections) rewritten while the
+        parameters, moments and outputs stay where they were.  (torch's
+        Optimizer step hooks and profiler annotation are not run: step is
+        marked hooked, see below.)"""
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        self._launch(self._begin())
+        plan, per_step = [], []
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            eps, lr = group["eps"], group["lr"]
+            for p in group["params"]:
+                g = p.grad
+                if g is None:
+                    continue
+                if not g.is_contiguous():
+                    raise RuntimeError("FusedAdam needs contiguous gradients")
+                st = self.state[p]
+                if not st:
+                    if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+                        raise RuntimeError("FusedAdam needs contiguous fp32 HIP tensors")
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                st["step"] += 1
+                t = st["step"]
+                out = self.param_out.get(p)
+                plan.append((p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                             out.data_ptr() if out is not None else 0, p.numel(), float(b1), float(b2), float(eps)))
+                per_step.append((g, float(lr), 1.0 - b1 ** t, (1.0 - b2 ** t) ** 0.5))
+        key = tuple(plan)
+        cached = getattr(self, "_plan_cache", None)
+        if cached is None or cached[0] != key:
+            launches = []
+            by_betas = {}
+            for i, d in enumerate(plan):
+                by_betas.setdefault(d[5:8], []).append(i)
+            for (b1, b2, eps), idx in by_betas.items():
+                for j in range(0, len(idx), N.GS_ADAM_MAX_TENSORS):
+                    chunk = idx[j:j + N.GS_ADAM_MAX_TENSORS]
+                    a = N.GsAdamArgs()
+                    a.num_tensors, a.beta1, a.beta2, a.eps = len(chunk), b1, b2, eps
+                    for k, i in enumerate(chunk):
+                        pp, m, v, o, num = plan[i][:5]
+                        a.t[k] = N.GsAdamTensor(pp, m, v, None, num, 0.0, 1.0, 1.0, o or None)
+                    launches.append((a, chunk))
+            cached = self._plan_cache = (key, launches)
+        lib = N.load()
+        stream = N.stream_ptr()
+        for a, chunk in cached[1]:
+            for k, i in enumerate(chunk):
+                g, lr, bc1, bc2s = per_step[i]
+                tk = a.t[k]
+                tk.grad, tk.lr, tk.bias_correction1, tk.bias_correction2_sqrt = g.data_ptr(), lr, bc1, bc2s
+            N.check(lib.gs_adam_step(C.byref(a), stream), "gs_adam_step")
         return loss
+
+    # torch.optim.Optimizer wraps step with its hook / profiler dispatch unless
+    # the function says it is hooked already: ~40 us of host time per step,
+    # which the small configurations are bound by
+    step.hooked = True
 
     @torch.no_grad()
     def step_ranges(self, ranges, before=None):

@@ -177,27 +177,51 @@ class StageTimer:
     enabled = False
     only = None  # optional set of stage names to record (the others cost nothing)
     events: list = []
+    pairs: list = []  # (name, e0, e1): intervals recorded around one launch (pair())
+    _pool: list = []  # created events, reused across resets (creating one costs more host time than recording)
+    _used = 0
+
+    @classmethod
+    def _event(cls):
+        if cls._used == len(cls._pool):
+            cls._pool.append(torch.cuda.Event(enable_timing=True))
+        e = cls._pool[cls._used]
+        cls._used += 1
+        return e
 
     @classmethod
     def mark(cls, name: str):
         if cls.enabled and (cls.only is None or name in cls.only):
-            e = torch.cuda.Event(enable_timing=True)
+            e = cls._event()
             e.record()
             cls.events.append((name, e))
 
     @classmethod
+    def pair(cls, name: str):
+        """(e0, e1) for a launch the library brackets itself (the frame
+        backward's blend launch), or None when `name` is not timed."""
+        if not (cls.enabled and (cls.only is None or name in cls.only)):
+            return None
+        e0, e1 = cls._event(), cls._event()
+        cls.pairs.append((name, e0, e1))
+        return e0, e1
+
+    @classmethod
     def reset(cls):
-        cls.events = []
+        cls.events, cls.pairs, cls._used = [], [], 0
 
     @classmethod
     def durations_ms(cls):
-        """{stage: [ms per occurrence]} -- stage = interval from its mark to the next."""
+        """{stage: [ms per occurrence]} -- stage = interval from its mark to
+        the next, or a bracketed launch's own interval."""
         torch.cuda.synchronize()
         out = {}
         ev = cls.events
         for (name, e0), (_, e1) in zip(ev[:-1], ev[1:]):
             if name.startswith("~"):
                 continue
+            out.setdefault(name, []).append(e0.elapsed_time(e1))
+        for name, e0, e1 in cls.pairs:
             out.setdefault(name, []).append(e0.elapsed_time(e1))
         return out
 
@@ -870,10 +894,11 @@ def _backward_frame(cam: CameraParams, fr: _FastFrame, xyz, cov3d, scaling, rota
     ba.d_xyz, ba.d_cov3d, ba.d_scaling, ba.d_rotation = N.ptr(d_xyz), N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot)
     ba.d_color_logits, ba.d_opacity, ba.d_sh_rest = N.ptr(d_col), N.ptr(d_op), N.ptr(d_sh)
     ba.project = 1 if chunks == 1 else 0
-    StageTimer.mark("blend_bwd")
+    ev = StageTimer.pair("blend_bwd")
+    if ev is not None:
+        ba.blend_events[0], ba.blend_events[1] = ev[0].cuda_event, ev[1].cuda_event
     N.check(lib.gs_render_backward(C.byref(ba), s), "gs_render_backward")
     if chunks == 1:
-        StageTimer.mark("~end_bwd")
         if rows_ready is not None:
             rows_ready(0, n)
         return d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh
@@ -885,12 +910,10 @@ def _backward_frame(cam: CameraParams, fr: _FastFrame, xyz, cov3d, scaling, rota
                             None, N.ptr(gm),
                             N.ptr(gc), N.ptr(d_xyz), N.ptr(d_cov), N.ptr(d_scl), N.ptr(d_rot), N.ptr(d_col),
                             N.ptr(d_op), N.ptr(d_sh), None, ba.grad_sums if pair_grads is not None else None, 0)
-    StageTimer.mark("project_bwd")
     bounds = [n * k // chunks for k in range(chunks + 1)]
     for lo, hi in zip(bounds[:-1], bounds[1:]):
         N.check(lib.gs_project_backward(C.byref(_rows_of(pb, lo, hi)), s), "gs_project_backward")
         rows_ready(lo, hi)
-    StageTimer.mark("~end_bwd")
     return d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh
 
 

@@ -508,6 +508,65 @@ def test_emit_capacity_guess(pkg, cuda):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("guess", ["last", 16])
+def test_frame_entry_points_match(pkg, cuda, guess):
+    """The default tile renders through the frame entry points
+    (gs_render_forward / gs_render_backward, one library call per direction);
+    the stage-by-stage path (GS_FRAME_CALLS=0, every other tile size) launches
+    the same kernels: outputs, gradients and the frame's index work are
+    bit-identical -- with a capacity guess that holds, and one far too small
+    (GS_NEED_CAPACITY, then the call resumed with a larger tile workspace)."""
+    RZ = pkg.rasterizer
+    syn = pkg.synthetic
+    sc = syn.make_scene(40000, 480, 270, seed=8, sigma_range=(0.002, 0.02))
+    res = []
+    saved = RZ._FRAME_CALLS
+    try:
+        for fast in (False, True):
+            RZ._FRAME_CALLS = fast
+            m = syn.to_model(sc, pkg.GaussianModel, cuda)
+            if guess != "last":
+                RZ._T_SEEN[cuda] = guess
+            out = pkg.GaussianRenderer().render(Cam(480, 270, sc.fovx, sc.fovy), m,
+                                                pkg.RenderSettings(270, 480, torch.tensor([0.1, 0.2, 0.3])))
+            (out["image"].sum() + out["alpha"].mean() + out["depth"].mean() + out["viewspace_points"].sum()).backward()
+            res.append([out[k].clone() for k in ("image", "alpha", "depth", "viewspace_points", "radii", "conics",
+                                                 "visibility_filter")] +
+                       [m._xyz.grad.clone(), m._scaling.grad.clone(), m._rotation.grad.clone(),
+                        m._features_dc.grad.clone(), m._opacity.grad.clone()])
+    finally:
+        RZ._FRAME_CALLS = saved
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_frame_entry_points_data_parallel_ranges(pkg, cuda):
+    """The frame backward with the data-parallel reduction's row ranges
+    (projection backward per range, gs_render_backward project = 0) equals
+    the one-range backward bit for bit."""
+    RZ = pkg.rasterizer
+    syn = pkg.synthetic
+    sc = syn.make_scene(20000, 320, 240, seed=9, sigma_range=(0.002, 0.02))
+    got = []
+    for chunks in (1, 3):
+        m = syn.to_model(sc, pkg.GaussianModel, cuda)
+        cam = pkg.camera_params(Cam(320, 240, sc.fovx, sc.fovy), pkg.RenderSettings(240, 320, torch.zeros(3)))
+        raw = (m._xyz, None, m._scaling, m._rotation, m._features_dc[:, 0, :], m._opacity)
+        with torch.no_grad():
+            img, al, dp, m2, cn, rd, vi, fr = RZ.forward_pipeline(cam, *[None if t is None else t.detach() for t in raw],
+                                                                  opacity_is_logit=True, need_grad=True)
+        assert isinstance(fr, RZ._FastFrame)
+        seen = []
+        out = {"_rows_ready": lambda lo, hi: seen.append((lo, hi)), "_chunks": chunks}
+        g = torch.ones_like(img)
+        d = RZ.backward_pipeline(cam, fr, *[None if t is None else t.detach() for t in raw], m2, cn, g, None, None,
+                                 None, None, opacity_is_logit=True, out=out)
+        assert seen == [(20000 * k // chunks, 20000 * (k + 1) // chunks) for k in range(chunks)]
+        got.append([t.clone() for t in d if t is not None])
+    for a, b in zip(*got):
+        assert torch.equal(a, b)
+
+
 def test_fused_adam_matches_torch_adam(pkg, cuda):
     """FusedAdam (one gs_adam_step launch) vs torch.optim.Adam, 5 groups as in
     the reference's GaussianOptimizer (optimizer.py:100-113), one param without grad."""
