@@ -302,19 +302,46 @@ def ptr(t) -> int:
 _HIP = None
 
 
-def host_device_pointer(host: "torch.Tensor"):
-    """The device address of a pinned host tensor (hipHostGetDevicePointer on
-    the HIP runtime torch loaded), or None if the runtime does not map it --
-    the caller then copies through the stream instead."""
+def _hip():
     global _HIP
-    if not host.is_pinned():
-        return None
     if _HIP is None:
         tl = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
         _HIP = C.CDLL(tl if os.path.exists(tl) else "libamdhip64.so.7")
         _HIP.hipHostGetDevicePointer.argtypes = [C.POINTER(_vp), _vp, C.c_uint]
         _HIP.hipHostGetDevicePointer.restype = C.c_int
+        _HIP.hipEventCreate.argtypes = [C.POINTER(_vp)]
+        _HIP.hipEventCreate.restype = C.c_int
+        _HIP.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), _vp, _vp]
+        _HIP.hipEventElapsedTime.restype = C.c_int
+    return _HIP
+
+
+class RawEvent:
+    """A hipEvent_t made on the HIP runtime torch loaded, for launches the
+    library brackets itself (gs_render_bwd_args.blend_events): torch's Event
+    objects do not know of a record made outside torch."""
+    __slots__ = ("handle",)
+
+    def __init__(self):
+        h = _vp()
+        if _hip().hipEventCreate(C.byref(h)) != 0:
+            raise RuntimeError("hipEventCreate failed")
+        self.handle = h.value
+
+    def elapsed_ms(self, end: "RawEvent") -> float:
+        ms = C.c_float(0.0)
+        if _hip().hipEventElapsedTime(C.byref(ms), _vp(self.handle), _vp(end.handle)) != 0:
+            raise RuntimeError("hipEventElapsedTime failed (both events recorded and complete?)")
+        return float(ms.value)
+
+
+def host_device_pointer(host: "torch.Tensor"):
+    """The device address of a pinned host tensor (hipHostGetDevicePointer on
+    the HIP runtime torch loaded), or None if the runtime does not map it --
+    the caller then copies through the stream instead."""
+    if not host.is_pinned():
+        return None
     d = _vp()
-    if _HIP.hipHostGetDevicePointer(C.byref(d), _vp(host.data_ptr()), 0) != 0 or not d.value:
+    if _hip().hipHostGetDevicePointer(C.byref(d), _vp(host.data_ptr()), 0) != 0 or not d.value:
         return None
     return int(d.value)

@@ -177,9 +177,11 @@ class StageTimer:
     enabled = False
     only = None  # optional set of stage names to record (the others cost nothing)
     events: list = []
-    pairs: list = []  # (name, e0, e1): intervals recorded around one launch (pair())
+    pairs: list = []  # (name, e0, e1): intervals the library records around one launch (pair())
     _pool: list = []  # created events, reused across resets (creating one costs more host time than recording)
     _used = 0
+    _raw: list = []   # N.RawEvent pool for pair()
+    _raw_used = 0
 
     @classmethod
     def _event(cls):
@@ -202,13 +204,16 @@ class StageTimer:
         backward's blend launch), or None when `name` is not timed."""
         if not (cls.enabled and (cls.only is None or name in cls.only)):
             return None
-        e0, e1 = cls._event(), cls._event()
+        while len(cls._raw) < cls._raw_used + 2:
+            cls._raw.append(N.RawEvent())
+        e0, e1 = cls._raw[cls._raw_used], cls._raw[cls._raw_used + 1]
+        cls._raw_used += 2
         cls.pairs.append((name, e0, e1))
         return e0, e1
 
     @classmethod
     def reset(cls):
-        cls.events, cls.pairs, cls._used = [], [], 0
+        cls.events, cls.pairs, cls._used, cls._raw_used = [], [], 0, 0
 
     @classmethod
     def durations_ms(cls):
@@ -222,7 +227,7 @@ class StageTimer:
                 continue
             out.setdefault(name, []).append(e0.elapsed_time(e1))
         for name, e0, e1 in cls.pairs:
-            out.setdefault(name, []).append(e0.elapsed_time(e1))
+            out.setdefault(name, []).append(e0.elapsed_ms(e1))
         return out
 
 
@@ -896,7 +901,7 @@ def _backward_frame(cam: CameraParams, fr: _FastFrame, xyz, cov3d, scaling, rota
     ba.project = 1 if chunks == 1 else 0
     ev = StageTimer.pair("blend_bwd")
     if ev is not None:
-        ba.blend_events[0], ba.blend_events[1] = ev[0].cuda_event, ev[1].cuda_event
+        ba.blend_events[0], ba.blend_events[1] = ev[0].handle, ev[1].handle
     N.check(lib.gs_render_backward(C.byref(ba), s), "gs_render_backward")
     if chunks == 1:
         if rows_ready is not None:
