@@ -208,7 +208,10 @@ def main():
                 p.grad = None
         out = renderer.render(cam, model, settings)
         torch.autograd.backward([out["image"], out["alpha"], out["depth"]], cot)
-        if reducer is not None and opt is not None:
+        if step.no_collective:  # (collective_share's reference run)
+            if opt is not None:
+                opt.step()
+        elif reducer is not None and opt is not None:
             reducer.reduce_and_step(opt)  # (pipelined per range when the backward handed over ranges)
         elif reducer is not None:
             reducer.all_reduce_mean()
@@ -216,6 +219,7 @@ def main():
             opt.step()
         frames.append(out)
 
+    step.no_collective = False
     for _ in range(a.spinup_steps + a.warmup):
         step()
         frames.clear()
@@ -244,6 +248,7 @@ def main():
         dt = float(t.item())
     StageTimer.only = None
     StageTimer.reset()
+    coll = collective_share(a, dist, dev, reducer, model, step, frames, dt) if reducer is not None else None
     # the per-stage breakdown from the stage-by-stage path (the same kernels;
     # the frame entry points would time only the blend backward)
     from mini3dgs_amd import rasterizer as _RZ
@@ -347,18 +352,76 @@ def main():
             "psnr_vs_ref": psnr,
         }
         if reducer is not None:
-            nsteps = a.spinup_steps + a.warmup + a.steps + a.diag_steps
+            nsteps = a.spinup_steps + a.warmup + 3 * a.steps + a.diag_steps
             line["allreduce"] = {"ranges_per_step": reducer.overlap_chunks(), "pipelined_adam": opt is not None,
                                  "host_us_per_step": {k: round(1e6 * v / nsteps, 1) for k, v in reducer.host_s.items()},
                                  "avg": reducer._avg, "native": reducer.native_status["native"],
                                  "rccl_nranks": reducer.native_status["rccl_nranks"],
                                  "self_check_err": reducer.native_status["self_check_err"],
                                  "fallback_reason": reducer.native_status["fallback_reason"]}
+            line["allreduce"].update(coll)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
         pkg.distributed.close_native_comms()
         dist.destroy_process_group()
+
+
+def timed_steps(dist, dev, k, fn):
+    """Wall seconds of k calls of fn, barrier + synchronize on both sides,
+    max over ranks (the contract's timing, for the extra measurements)."""
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        fn()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def collective_share(a, dist, dev, reducer, model, step, frames, dt):
+    """The all-reduce's part of the timed step (N > 1, or --force-dist), from
+    two extra runs of --steps steps after the timed region:
+      * the same steps with an event pair on the collective stream around
+        each range's collective: gpu_us_per_step = their summed durations per
+        step (max over ranks; native RCCL only -- torch.distributed's
+        collectives run on streams or threads this process cannot time);
+      * the same steps without the collective (the gradients stay local, the
+        Adam step reads them unreduced): exposed_frac = (timed step - that
+        step) / timed step, the share of the step the collective adds."""
+    k = a.steps
+    timed = reducer.set_timing(True)
+    dt_coll = timed_steps(dist, dev, k, lambda: (step(), frames.clear()))
+    ms = reducer.collective_gpu_ms() if timed else None
+    reducer.set_timing(False)
+    per_step = sum(ms) / k if ms else (0.0 if timed else -1.0)
+    t = torch.tensor([per_step], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per_step = float(t.item())
+    model._gs_grad_sink, sink = None, model._gs_grad_sink  # the backward writes local .grad tensors
+    step.no_collective = True
+    try:
+        dt_nc = timed_steps(dist, dev, k, lambda: (step(), frames.clear()))
+    finally:
+        step.no_collective = False
+        model._gs_grad_sink = sink
+    return {"gpu_us_per_step": round(1e3 * per_step, 1) if per_step >= 0 else None,
+            "collectives_per_step": (len(ms) / k if ms else None),
+            "gpu_us_note": "event pair on the native RCCL stream per collective, max over ranks" if timed
+            else "not measurable: the collectives run through torch.distributed (" + reducer.native_status[
+                "fallback_reason"] + ")",
+            "ms_per_step_timing_run": round(1e3 * dt_coll / k, 4),
+            "ms_per_step_no_collective": round(1e3 * dt_nc / k, 4),
+            "exposed_frac": round(max(0.0, dt - dt_nc) / dt, 4),
+            "exposed_note": "(timed step - the same run's step without the all-reduce) / timed step"}
 
 
 def pmc_traffic(stage):

@@ -258,6 +258,22 @@ class GradAllReduce:
         self._works.append((lo, hi, [self.dist.all_reduce(t, op=op, group=self.group, async_op=True)
                                      for t in slices]))
 
+    def set_timing(self, on: bool) -> bool:
+        """Time each collective on the GPU from now on (True) or stop (False);
+        returns whether this bucket can: native RCCL only, whose collective
+        stream is this process's own (torch.distributed runs RCCL on streams
+        it does not expose, gloo on host threads)."""
+        if self._native is None:
+            return False
+        self._native.collective_ms(reset=True)
+        self._native.timing = bool(on)
+        return True
+
+    def collective_gpu_ms(self) -> Optional[List[float]]:
+        """GPU milliseconds of each collective issued since set_timing(True),
+        in issue order (waits for them); None where set_timing cannot time."""
+        return self._native.collective_ms(reset=True) if self._native is not None else None
+
     def covers(self, leaves) -> bool:
         """Do `leaves` write every parameter of the bucket?  Only then may the
         backward hand rows to rows_ready (a parameter no kernel writes would

@@ -865,8 +865,8 @@ def _backward_frame(cam: CameraParams, fr: _FastFrame, xyz, cov3d, scaling, rota
     ba = N.GsRenderBwdArgs()
     fa = fr.fa
     ba.cam, ba.fb, ba.M, ba.T, ba.tile_alt = fa.cam, fa.fb, fr.M, fr.T, fa.tile_alt
-    ba.g = _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest, sh_degree)
-    ba.means2d, ba.conics, ba.vis = means2d.data_ptr(), conics.data_ptr(), fa.vis
+    # (the forward's Gaussians: the tensors autograd saved for this backward)
+    ba.g, ba.means2d, ba.conics, ba.vis = fa.g, fa.means2d, fa.conics, fa.vis
     pair_grads = None
     if fr.M > 0 and fr.T > 0 and pixel_grads:
         if g_image is None:
@@ -980,7 +980,7 @@ class RasterizeGaussians(torch.autograd.Function):
                 d_cov if (cov3d is not None and need[1]) else None,
                 d_scl if (scaling is not None and need[2]) else None,
                 d_rot if (rotation is not None and need[3]) else None,
-                d_col if need[4] else None,
+                d_col.view(logits.shape) if need[4] else None,
                 d_op.view(opacity.shape) if need[5] else None,
                 d_sh if (sh_rest is not None and need[6]) else None,
                 None, None, None, None)

@@ -100,8 +100,10 @@ def _libs():
         hip.hipStreamWaitEvent.argtypes = [vp, vp, C.c_uint]
         hip.hipEventDestroy.argtypes = [vp]
         hip.hipEventQuery.argtypes = [vp]
+        hip.hipEventSynchronize.argtypes = [vp]
+        hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), vp, vp]
         for f in ("hipEventCreateWithFlags", "hipEventRecord", "hipStreamWaitEvent", "hipEventDestroy",
-                  "hipEventQuery"):
+                  "hipEventQuery", "hipEventSynchronize", "hipEventElapsedTime"):
             getattr(hip, f).restype = C.c_int
         _LIBS = (rccl, hip)
     return _LIBS
@@ -144,6 +146,13 @@ class RcclComm:
         self._comm = C.c_void_p()
         self._ready: List[C.c_void_p] = []
         self._done: List[C.c_void_p] = []
+        # collective GPU time (diagnostic, off by default): a timing event pair
+        # on the collective stream around each range's ncclGroupStart..End,
+        # i.e. the collective's own execution, not its wait for the compute
+        # stream's "ready" event (set_timing / collective_ms)
+        self.timing = False
+        self._tpool: List[Tuple[C.c_void_p, C.c_void_p]] = []
+        self._tpairs: List[Tuple[C.c_void_p, C.c_void_p]] = []
         self._stream = None
         self.nranks = None
         self.self_check = None
@@ -231,9 +240,9 @@ class RcclComm:
             finally:
                 self._comm = C.c_void_p()
         if hip is not None:
-            for ev in self._ready + self._done:
+            for ev in self._ready + self._done + [e for p in self._tpool + self._tpairs for e in p]:
                 hip.hipEventDestroy(ev)
-        self._ready, self._done = [], []
+        self._ready, self._done, self._tpool, self._tpairs = [], [], [], []
 
     def _events(self, k: int):
         while len(self._ready) <= k:
@@ -254,6 +263,9 @@ class RcclComm:
         _check_hip(hip.hipEventRecord(ready, comp), "hipEventRecord")
         _check_hip(hip.hipStreamWaitEvent(coll, ready, 0), "hipStreamWaitEvent")
         op = NCCL_AVG if avg else NCCL_SUM
+        tp = self._timing_pair() if self.timing else None
+        if tp is not None:
+            _check_hip(hip.hipEventRecord(tp[0], coll), "hipEventRecord")
         group = len(pieces) > 1
         if group:
             _check_nccl(rccl, rccl.ncclGroupStart(), "ncclGroupStart")
@@ -265,7 +277,32 @@ class RcclComm:
         finally:
             if group:
                 _check_nccl(rccl, rccl.ncclGroupEnd(), "ncclGroupEnd")
+        if tp is not None:
+            _check_hip(hip.hipEventRecord(tp[1], coll), "hipEventRecord")
+            self._tpairs.append(tp)
         _check_hip(hip.hipEventRecord(done, coll), "hipEventRecord")
+
+    def _timing_pair(self):
+        if self._tpool:
+            return self._tpool.pop()
+        pair = (C.c_void_p(), C.c_void_p())
+        for ev in pair:
+            _check_hip(self._hip.hipEventCreateWithFlags(C.byref(ev), 0), "hipEventCreate")
+        return pair
+
+    def collective_ms(self, reset: bool = True) -> List[float]:
+        """GPU milliseconds of each collective issued since the last reset
+        while `timing` was on (waits for them), in issue order."""
+        out = []
+        for t0, t1 in self._tpairs:
+            _check_hip(self._hip.hipEventSynchronize(t1), "hipEventSynchronize")
+            ms = C.c_float(0.0)
+            _check_hip(self._hip.hipEventElapsedTime(C.byref(ms), t0, t1), "hipEventElapsedTime")
+            out.append(float(ms.value))
+        if reset:
+            self._tpool.extend(self._tpairs)
+            self._tpairs = []
+        return out
 
     def wait_done(self, k: int, timeout_s: float) -> None:
         """The host waits (polling) for range k's collective, at most timeout_s."""
@@ -290,6 +327,6 @@ class RcclComm:
             torch.cuda.synchronize(self.device)
             self._rccl.ncclCommDestroy(self._comm)
             self._comm = C.c_void_p()
-        for ev in self._ready + self._done:
+        for ev in self._ready + self._done + [e for p in self._tpool + self._tpairs for e in p]:
             self._hip.hipEventDestroy(ev)
-        self._ready, self._done = [], []
+        self._ready, self._done, self._tpool, self._tpairs = [], [], [], []

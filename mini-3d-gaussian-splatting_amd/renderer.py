@@ -76,15 +76,24 @@ def effective_tile(tile_size: int, width: int, height: int) -> int:
     return t
 
 
+def _host_f32(t, count: int) -> list:
+    """The values of `t` (a tensor or sequence of `count` numbers) rounded to
+    fp32, as Python floats, row-major (a CPU fp32 tensor is read as is)."""
+    t = torch.as_tensor(t)
+    if t.device.type != "cpu" or t.dtype != torch.float32:
+        t = t.detach().to("cpu", torch.float32)
+    if t.numel() != count:
+        raise ValueError(f"expected {count} values, got a tensor of shape {tuple(t.shape)}")
+    return t.reshape(count).tolist()
+
+
 def camera_params(camera, settings: RenderSettings, radius_min=0.01, radius_max=50.0, tile_size=16) -> CameraParams:
     """Host scalars of renderer.py:140-152 (python double -> fp32 in the ABI)."""
     W, H = camera._width, camera._height
     fx = 0.5 * W / math.tan(camera._FoVx * 0.5)
     fy = 0.5 * H / math.tan(camera._FoVy * 0.5)
-    wv = _world_view(camera).detach().to("cpu", torch.float32).reshape(4, 4)
-    view = tuple(float(v) for v in wv[:3, :].reshape(-1).tolist())
-    bg = settings.bg_color
-    bg = tuple(float(v) for v in torch.as_tensor(bg).detach().to("cpu", torch.float32).reshape(3).tolist())
+    view = tuple(_host_f32(_world_view(camera), 16)[:12])
+    bg = tuple(_host_f32(settings.bg_color, 3))
     tile = effective_tile(tile_size, settings.image_width, settings.image_height)
     return CameraParams(int(settings.image_width), int(settings.image_height), fx, fy, W * 0.5, H * 0.5,
                         view, bg, float(radius_min), float(radius_max), tile)
@@ -114,10 +123,11 @@ class GaussianRenderer:
         if fused:
             # this package's GaussianModel: covariance from the raw scaling /
             # rotation and get_opacity's sigmoid are computed in the kernels;
-            # squeeze (a view) keeps autograd from materialising a zero-filled
-            # [N,1,3] gradient as a select would
+            # the [N,1,3] / [N,1] leaves go in as they are (no view node on the
+            # tape: the rasterizer reads rows by stride and returns gradients
+            # in the leaves' shapes)
             cov3d, scaling, rotation = None, gaussians._scaling, gaussians._rotation
-            logits = gaussians._features_dc.squeeze(1)
+            logits = gaussians._features_dc
         else:
             cov3d, scaling, rotation = gaussians.get_covariance, None, None
             feats = gaussians.get_features  # one read: the SH rest below is a view of it
@@ -125,7 +135,7 @@ class GaussianRenderer:
                 logits = feats[:, 0, :]
             else:
                 logits = gaussians._features_dc.squeeze(1)
-        opacity = gaussians._opacity.squeeze(1) if fused else gaussians.get_opacity.squeeze(1)
+        opacity = gaussians._opacity if fused else gaussians.get_opacity.squeeze(1)
         sh_degree = settings.sh_degree
         if sh_degree is None:
             sh_degree = int(getattr(gaussians, "active_sh_degree", 0))

@@ -14,6 +14,9 @@ for c in C1 C2 C3 4K; do
 done
 timeout -k 10 200 python tools/host_profile.py 5000 256 256 500 > "$O/hostprof_c1.log" 2>&1 || exit 1
 head -3 "$O/hostprof_c1.log"
+timeout -k 10 200 python tools/host_split.py 5000 256 256 500 > "$O/hostsplit_c1.log" 2>&1 || exit 1
+timeout -k 10 200 python tools/host_split.py 100000 800 800 300 > "$O/hostsplit_c2.log" 2>&1 || exit 1
+cat "$O/hostsplit_c1.log" "$O/hostsplit_c2.log" | grep -v amdgpu.ids
 cd /tmp && export TMPDIR=/tmp
 for c in C1 C2; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$c" -o run --output-format csv -- python3 "$R/bench.py" --config $c --steps 50 --warmup 5 --no-cpu-baseline > "$O/prof_$c.log" 2>&1 || { echo "rocprof $c failed"; exit 1; }
