@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 18
+#define GS_ABI_VERSION 19
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 4096      /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
                                  of at least max(W, H) renders the same as any larger one (one tile
@@ -312,6 +312,20 @@ typedef struct gs_blend_bwd_args {
   int32_t cell_count;           /* the batch's cells (0: gs_tile_quads(tile_size), the whole tile) */
 } gs_blend_bwd_args;
 gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream);
+/* Diagnostic (SURVEY 8(d) lane efficiency; not on the render path): the same
+ * replay as gs_blend_backward at the default tile (one batch), counting its
+ * phase-A lanes.  hist: device [2][65] uint64, added to -- per replayed
+ * (entry, cell), [0][r] counts replays entered by r running lanes (lanes of
+ * the cell's pixels whose transmittance has not terminated), [1][c] replays
+ * where c lanes' pairs contribute (weight > 0).  per_group: device [G][4]
+ * uint32 overwritten, G = gs_blend_backward_groups(tiles_x, tiles_y, 4),
+ * workgroup b = (tile, cell) per gs_blend_backward's grid: replays, replays
+ * entered with >= 32 running lanes, sum of running lanes, sum of
+ * contributing lanes (empty workgroups: zeros).  The gradient partials are
+ * written as by gs_blend_backward. */
+int64_t gs_blend_backward_groups(int32_t tiles_x, int32_t tiles_y, int32_t cell_count);
+gs_status gs_blend_backward_lane_stats(const gs_blend_bwd_args *a, uint64_t *hist, uint32_t *per_group,
+                                       gs_stream_t stream);
 
 /* ---- Backward of the projection ----------------------------------------
  * Sums each Gaussian's slot partials (slots [pair_offset[g], pair_offset[g]

@@ -27,7 +27,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 18
+GS_ABI_VERSION = 19
 GS_NEED_CAPACITY, GS_RETRY_FULL_KEYS = 4, 5  # gs_render_forward: what to do next (not errors)
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
@@ -189,7 +189,7 @@ EXPORTS = (
     "gs_abi_version", "gs_last_error", "gs_project_forward", "gs_radix_sort_workspace_bytes",
     "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
     "gs_tile_ranges", "gs_blend_live_words", "gs_tile_quads", "gs_partial_groups", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-    "gs_gather_partials", "gs_frame_workspace_bytes", "gs_tile_workspace_bytes", "gs_render_forward",
+    "gs_blend_backward_groups", "gs_blend_backward_lane_stats", "gs_gather_partials", "gs_frame_workspace_bytes", "gs_tile_workspace_bytes", "gs_render_forward",
     "gs_render_backward", "gs_frame_offsets", "gs_tile_offsets", "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
     "gs_densify_workspace_bytes", "gs_densify_count", "gs_densify_emit",
 )
@@ -226,6 +226,9 @@ def _declare(lib):
     lib.gs_partial_groups.restype = C.c_int32
     lib.gs_blend_forward.argtypes = [P(GsBlendFwdArgs), _vp]
     lib.gs_blend_backward.argtypes = [P(GsBlendBwdArgs), _vp]
+    lib.gs_blend_backward_groups.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    lib.gs_blend_backward_groups.restype = C.c_int64
+    lib.gs_blend_backward_lane_stats.argtypes = [P(GsBlendBwdArgs), _vp, _vp, _vp]
     lib.gs_project_backward.argtypes = [P(GsProjectBwdArgs), _vp]
     lib.gs_gather_partials.argtypes = [P(GsProjectBwdArgs), C.c_int32, _vp]
     lib.gs_frame_workspace_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32]
@@ -248,8 +251,8 @@ def _declare(lib):
     lib.gs_densify_count.argtypes = [P(GsDensifyArgs), _vp]
     lib.gs_densify_emit.argtypes = [P(GsDensifyArgs), _vp]
     for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_count", "gs_bin_emit",
-              "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
-              "gs_gather_partials", "gs_render_forward", "gs_render_backward", "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
+              "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_blend_backward_lane_stats",
+              "gs_project_backward", "gs_gather_partials", "gs_render_forward", "gs_render_backward", "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
         getattr(lib, f).restype = C.c_int
 
 

@@ -187,6 +187,12 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   ba.capacity = a->fb.capacity;
   ba.tile_keys = a->fb.capacity > 0 ? reinterpret_cast<uint32_t *>(tw + T0.tk[0]) : nullptr;
   ba.pair_gauss = a->fb.capacity > 0 ? reinterpret_cast<uint32_t *>(tw + T0.tv[0]) : nullptr;
+  // the tile sort's first-pass digit counts come from the emission (the
+  // count clears their table in the tile sort's workspace): one histogram
+  // kernel less
+  const int32_t bits = tiles > 1 ? 32 - __builtin_clz((uint32_t)(tiles - 1)) : 1;
+  const int32_t bits0 = gs_internal_first_pass_bits(0, bits);
+  uint32_t *tile_counts = a->fb.capacity > 0 ? reinterpret_cast<uint32_t *>(tw + T0.sort_ws) : nullptr;
   if (!a->resume) {
     // the counts, then -- with a capacity guess -- the emission, queued before
     // the host reads (M, T) back: its kernel time hides the read-back
@@ -194,8 +200,8 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
     ba.host_seq = a->host_seq;
     volatile uint32_t *hc = a->host_counters_host;
     hc[4] = 0u;  // (the previous frame's sequence word)
-    if ((st = gs_bin_count(&ba, stream))) return st;
-    if (a->fb.capacity > 0 && (st = gs_bin_emit(&ba, stream))) return st;
+    if ((st = gs_internal_bin_count_hist(&ba, tile_counts, bits0, stream))) return st;
+    if (a->fb.capacity > 0 && (st = gs_internal_bin_emit_hist(&ba, tile_counts, bits0, stream))) return st;
     // the one host synchronisation of a frame: poll the sequence word the
     // count writes through the pinned buffer's device address (no event, no copy)
     const auto t0 = std::chrono::steady_clock::now();
@@ -218,15 +224,17 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   } else {
     if ((int64_t)a->T > a->fb.capacity)
       return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: resume needs a capacity of at least T", what);
-    if ((st = gs_bin_emit(&ba, stream))) return st;
+    const size_t words = ((size_t)1 << bits0) * (((size_t)a->fb.capacity + kSortBlockEntries - 1) / kSortBlockEntries);
+    if (hipMemsetAsync(tile_counts, 0, 4 * words, (hipStream_t)stream) != hipSuccess)
+      return gs_internal_fail(GS_ERR_LAUNCH, "%s: count table memset failed", what);
+    if ((st = gs_internal_bin_emit_hist(&ba, tile_counts, bits0, stream))) return st;
   }
   const int32_t T = a->T;
   int32_t talt = 0;
-  const int32_t bits = tiles > 1 ? 32 - __builtin_clz((uint32_t)(tiles - 1)) : 1;
   uint32_t *tk = reinterpret_cast<uint32_t *>(tw + T0.tk[0]), *tk1 = reinterpret_cast<uint32_t *>(tw + T0.tk[1]);
   uint32_t *tv = reinterpret_cast<uint32_t *>(tw + T0.tv[0]), *tv1 = reinterpret_cast<uint32_t *>(tw + T0.tv[1]);
-  if ((st = gs_radix_sort_pairs(tk, tv, tk1, tv1, T, 0, bits, 0, tw + T0.sort_ws,
-                                gs_radix_sort_workspace_bytes((int32_t)a->fb.capacity), &talt, stream)))
+  if ((st = gs_internal_radix_sort_pairs(tk, tv, tk1, tv1, T, 0, bits, 0, tw + T0.sort_ws,
+                                         gs_radix_sort_workspace_bytes((int32_t)a->fb.capacity), &talt, 1, stream)))
     return st;
   a->tile_alt = talt;
   gs_range_args ra;

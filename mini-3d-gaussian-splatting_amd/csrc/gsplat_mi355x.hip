@@ -30,6 +30,7 @@ constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
 constexpr int kSortIpt = 8;                      // items per thread per sort block (4, 16: slower)
 constexpr int kSortChunk = kBlock * kSortIpt;    // 2048 items per block
+static_assert(kSortChunk == kSortBlockEntries, "gs_internal.h kSortBlockEntries");
 constexpr int kBinChunk = kBlock * 4;            // 1024 Gaussians per binning block (2 and 1 rounds: slower)
 #ifndef GS_DEBUG  // 1: report (printf) blend list ranges clamped to the T entries
 #define GS_DEBUG 0
@@ -730,8 +731,18 @@ __device__ __forceinline__ uint2 *sorted_rects(uint32_t *partials, int nb) {
 
 // partials[0..nb): touches per block (depth order), partials[nb..2nb): visible per index chunk,
 // [2nb..3nb): index-order slots per chunk, [3nb..5nb): depth-bits min / max per chunk
-__global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials, int nb) {
+// The tile sort's first-pass digit counts (k_radix_hist's table), built by
+// k_bin_emit as it writes the entries (gs_internal_bin_emit_hist): the
+// table, zeroed by k_bin_partials, the kernel before it in the stream.
+struct TileHist {
+  uint32_t *counts;     // [2^bits, nb_sort] (row d: digit d's count per sort block)
+  uint32_t zero_words;  // words k_bin_partials clears: 2^bits * div_up(capacity, kSortChunk)
+  int bits;             // first pass digit width (shift 0); 0: no table
+};
+
+__global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials, int nb, TileHist th) {
   __shared__ uint32_t s_tmp[4];
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < th.zero_words; i += gridDim.x * kBlock) th.counts[i] = 0u;
   const long long base = (long long)blockIdx.x * kBinChunk;
   constexpr int kR = kBinChunk / kBlock;
   // Loads unconditional (clamped index) and all rounds' at once: two round
@@ -916,17 +927,32 @@ __device__ __forceinline__ void wave_fill_runs(bool wide, uint32_t lo, uint32_t 
 }
 
 constexpr uint32_t kOwnerCap = kBlock * 64;
-__global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials) {
+// sort blocks a binning block's output may span with its digit counts in LDS
+// (a block emits ~4.5 K entries at C3, ~3 sort blocks); counts past them go
+// straight to the table
+constexpr int kHistSpan = 8;
+__global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials, TileHist th) {
   __shared__ uint32_t s_off[kBlock + 1];
   __shared__ uint32_t s_g[kBlock];
   __shared__ uint2 s_rect[kBlock];
   __shared__ uint32_t s_tmp[4];
   __shared__ uint8_t s_owner[kOwnerCap];
+  __shared__ uint32_t s_hist[kHistSpan * kRadix];
   // T entries do not fit: do nothing (the caller re-emits into T-sized
   // buffers; the slot pass below is not idempotent, so it must run once)
-  if ((long long)a.counters[1] > a.capacity) return;
+  const uint32_t T = a.counters[1];
+  if ((long long)T > a.capacity) return;
   const long long base = (long long)blockIdx.x * kBinChunk;
   uint32_t out_base = partials[blockIdx.x];
+  // first-pass digit counts of the entries this block writes: sort block
+  // (out_base + o) / kSortChunk, digit key & hmask (shift 0)
+  const bool hist = th.bits > 0;
+  const uint32_t hmask = (1u << th.bits) - 1u, nbs = (T + kSortChunk - 1) / kSortChunk;
+  const uint32_t hb0 = out_base / kSortChunk;
+  if (hist) {
+    for (int i = threadIdx.x; i < kHistSpan * kRadix; i += kBlock) s_hist[i] = 0u;
+    // (ordered before the first use by the barrier inside the first round's scan)
+  }
   constexpr int kR = kBinChunk / kBlock;
   // all rounds' ids and rects unconditionally (clamped): one round trip for
   // the block
@@ -979,11 +1005,27 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
         const uint32_t wt = (rr.x >> 16) - tx0 + 1u;
         const uint32_t loc = o - s_off[lo];
         const uint32_t row = loc / wt;
-        a.tile_keys[out_base + o] = (ty0 + row) * (uint32_t)a.tiles_x + tx0 + (loc - row * wt);
+        const uint32_t key = (ty0 + row) * (uint32_t)a.tiles_x + tx0 + (loc - row * wt);
+        a.tile_keys[out_base + o] = key;
         a.pair_gauss[out_base + o] = s_g[lo];
+        if (hist) {
+          const uint32_t sb = (out_base + o) / kSortChunk, d = key & hmask;
+          if (sb - hb0 < (uint32_t)kHistSpan)
+            atomicAdd(&s_hist[(sb - hb0) * kRadix + d], 1u);
+          else
+            atomicAdd(&th.counts[(size_t)d * nbs + sb], 1u);
+        }
       }
     }
     out_base += tot;
+  }
+  if (hist) {
+    __syncthreads();
+    // (integer sums: the table is the same whatever order the blocks add in)
+    for (int i = threadIdx.x; i < kHistSpan * kRadix; i += kBlock) {
+      const uint32_t v = s_hist[i], sb = hb0 + (uint32_t)(i / kRadix), d = (uint32_t)(i % kRadix);
+      if (v && sb < nbs && d <= hmask) atomicAdd(&th.counts[(size_t)d * nbs + sb], v);
+    }
   }
   // Gradient slots, in Gaussian-index order over this block's index chunk
   // (coalesced): the chunk's offset + each Gaussian's prefix in the chunk
@@ -1319,9 +1361,26 @@ __device__ __forceinline__ bool simple_entry(float4 r0, float4 r1) {
 // [T, cells] partial buffer too large; each batch's partials are summed by
 // gs_gather_partials before the next batch overwrites them).  kT16: the
 // default tile, one batch of its four cells.
-template <bool kT16>
-__global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
+// Phase-A lane statistics (gs_blend_backward_lane_stats; the kStats
+// instantiation only -- the product kernel carries none of it): per replayed
+// (entry, cell), the lanes still running into it and the lanes whose pair
+// contributes (c > 0), as two 65-bin histograms, and per workgroup the
+// replays, the replays entered with >= 32 running lanes, and the sums of
+// running and contributing lanes.
+struct BwdStats {
+  unsigned long long *hist;  // [2][65]: running lanes, contributing lanes per replay
+  uint32_t *per_group;       // [grid][4]
+};
+
+template <bool kT16, bool kStats = false>
+__global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdStats stats = {nullptr, nullptr}) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
+  __shared__ uint32_t s_hist[kStats ? 2 * 65 : 1];
+  uint32_t n_rep = 0, n_rep32 = 0, sum_run = 0, sum_con = 0;  // (kStats)
+  if constexpr (kStats) {
+    for (int i = threadIdx.x; i < 2 * 65; i += kWave) s_hist[i] = 0u;
+    if (threadIdx.x < 4) stats.per_group[(size_t)blockIdx.x * 4 + threadIdx.x] = 0u;
+  }
   __shared__ float4 s_pg[kWave];         // per pixel: dL/drgb (masked), dL/dD
   // the chunk's records (word 10 = slot), staged per chunk from registers:
   // 384 B instead of a word's 3 KB, for occupancy (LDS bounds it)
@@ -1566,6 +1625,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       // is the forward's "A < 0.995 before this entry", carried from the
       // previous entry's own test -- the same decisions as i < n_eval
       const bool live = run && !(sq > kSkipS);
+      uint32_t n_run = 0;
+      if constexpr (kStats) n_run = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(run));
       const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
       const bool simple = kAllSimple || ((simple_w >> bit) & 1ull);
       float dop, cw;
@@ -1615,6 +1676,17 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
       }
       s_dc[kk][lane] = make_float2(dop, cw);
       k = kk + 1;
+      if constexpr (kStats) {
+        const uint32_t n_con = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(cw != 0.f));
+        if (lane == 0) {
+          atomicAdd(&s_hist[n_run], 1u);
+          atomicAdd(&s_hist[65 + n_con], 1u);
+        }
+        n_rep += 1u;
+        n_rep32 += n_run >= 32u ? 1u : 0u;
+        sum_run += n_run;
+        sum_con += n_con;
+      }
      }
      if (kAllSimple || (simple_w & cm) == cm) phase_b(std::false_type{}, k); else phase_b(std::true_type{}, k);
      kb += (uint32_t)k;
@@ -1622,6 +1694,18 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a) {
     };
     if ((simple_w & mcur) == mcur) run_word(std::true_type{}); else run_word(std::false_type{});
     mcur = mnext;
+  }
+  if constexpr (kStats) {
+    __syncthreads();
+    if (lane == 0) {
+      uint32_t *pg = stats.per_group + (size_t)blockIdx.x * 4;
+      pg[0] = n_rep;
+      pg[1] = n_rep32;
+      pg[2] = sum_run;
+      pg[3] = sum_con;
+    }
+    for (int i = lane; i < 2 * 65; i += kWave)
+      if (s_hist[i]) atomicAdd(&stats.hist[i], (unsigned long long)s_hist[i]);
   }
 }
 
@@ -2144,6 +2228,16 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
                               int32_t n, int32_t begin_bit, int32_t end_bit, int32_t vals_are_iota,
                               void *workspace, size_t workspace_bytes, int32_t *result_in_alt,
                               gs_stream_t stream) {
+  return gs_internal_radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, begin_bit, end_bit, vals_are_iota,
+                                      workspace, workspace_bytes, result_in_alt, 0, stream);
+}
+
+}  // extern "C"
+
+gs_status gs_internal_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
+                                       int32_t n, int32_t begin_bit, int32_t end_bit, int32_t vals_are_iota,
+                                       void *workspace, size_t workspace_bytes, int32_t *result_in_alt,
+                                       int32_t first_counts_ready, gs_stream_t stream) {
   if (!result_in_alt) return fail(GS_ERR_INVALID_ARG, "%s: null result_in_alt", "gs_radix_sort_pairs");
   if (begin_bit < 0 || end_bit > 32 || begin_bit >= end_bit || n < 0)
     return fail(GS_ERR_INVALID_ARG, "%s: bad bit range / n", "gs_radix_sort_pairs");
@@ -2164,7 +2258,7 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
   int shift = begin_bit;
   for (int p = 0; p < passes; ++p) {
     const int nbits = (end_bit - shift + (passes - p) - 1) / (passes - p);
-    k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, nb);
+    if (p > 0 || !first_counts_ready) k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, nb);
     k_radix_scan<<<1 << nbits, kBlock, 0, s>>>(counts, totals, nb);
     if (p == 0 && vals_are_iota)
       k_radix_scatter<true><<<nb, kBlock, 0, s>>>(kin, nullptr, kout, vout, n, shift, nbits, counts, totals, nb);
@@ -2181,6 +2275,35 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
   }
   return GS_OK;
 }
+
+int32_t gs_internal_first_pass_bits(int32_t begin_bit, int32_t end_bit) {
+  const int passes = (end_bit - begin_bit + kRadixBits - 1) / kRadixBits;
+  return passes > 0 ? (end_bit - begin_bit + passes - 1) / passes : 0;
+}
+
+gs_status gs_internal_bin_count_hist(const gs_bin_args *a, uint32_t *tile_counts, int32_t bits, gs_stream_t stream) {
+  if (!a || !a->counters || a->n <= 0 || !a->workspace || a->workspace_bytes < gs_bin_workspace_bytes(a->n))
+    return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_internal_bin_count_hist");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)div_up(a->n, kBinChunk);
+  uint32_t *partials = (uint32_t *)a->workspace;
+  const uint32_t zero = tile_counts ? (uint32_t)((1u << bits) * div_up(a->capacity > 0 ? a->capacity : 0, kSortChunk))
+                                    : 0u;
+  k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials, nb, TileHist{tile_counts, zero, 0});
+  k_bin_scan_partials<<<1, kBlock, 0, s>>>(partials, nb, a->counters, a->host_counters, a->host_seq);
+  return check_launch("gs_bin_count");
+}
+
+gs_status gs_internal_bin_emit_hist(const gs_bin_args *a, uint32_t *tile_counts, int32_t bits, gs_stream_t stream) {
+  if (!a || a->n <= 0 || !tile_counts || bits < 1 || bits > kRadixBits)
+    return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_internal_bin_emit_hist");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)div_up(a->n, kBinChunk);
+  k_bin_emit<<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace, TileHist{tile_counts, 0u, bits});
+  return check_launch("gs_bin_emit");
+}
+
+extern "C" {
 
 gs_status gs_depth_sort_msd(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt, int32_t n,
                             int32_t key_bits, void *workspace, size_t workspace_bytes, uint32_t *overflow_word,
@@ -2220,7 +2343,7 @@ gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
   uint32_t *partials = (uint32_t *)a->workspace;
-  k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials, nb);
+  k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials, nb, TileHist{nullptr, 0u, 0});
   k_bin_scan_partials<<<1, kBlock, 0, s>>>(partials, nb, a->counters, a->host_counters, a->host_seq);
   return check_launch("gs_bin_count");
 }
@@ -2236,7 +2359,7 @@ gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream) {
   if (a->capacity < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative capacity", "gs_bin_emit");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
-  k_bin_emit<<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace);
+  k_bin_emit<<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace, TileHist{nullptr, 0u, 0});
   return check_launch("gs_bin_emit");
 }
 
@@ -2314,6 +2437,30 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   else
     k_blend_bwd<false><<<(unsigned)blocks, kWave, 0, s>>>(b);
   return check_launch("gs_blend_backward");
+}
+
+int64_t gs_blend_backward_groups(int32_t tiles_x, int32_t tiles_y, int32_t cell_count) {
+  if (tiles_x <= 0 || tiles_y <= 0 || cell_count <= 0) return 0;
+  return (int64_t)div_up(tiles_x * tiles_y, 8) * 8LL * cell_count;
+}
+
+gs_status gs_blend_backward_lane_stats(const gs_blend_bwd_args *a, uint64_t *hist, uint32_t *per_group,
+                                       gs_stream_t stream) {
+  if (!a || !hist || !per_group) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_backward_lane_stats");
+  if (a->cam.tile_size != GS_DEFAULT_TILE || !(a->cell_begin == 0 && (a->cell_count == 0 || a->cell_count == 4)))
+    return fail(GS_ERR_UNSUPPORTED, "%s: the default tile, one batch", "gs_blend_backward_lane_stats");
+  if (!a->ranges || !a->sorted_gauss || !a->records || !a->pix_acc || !a->pix_state || !a->g_image ||
+      !a->pair_grads || !a->slot_live || !tiles_match(a->cam, a->tiles_x, a->tiles_y))
+    return fail(GS_ERR_INVALID_ARG, "%s: bad buffers", "gs_blend_backward_lane_stats");
+  gs_blend_bwd_args b = *a;
+  b.cell_begin = 0;
+  b.cell_count = 4;
+  const int64_t blocks = gs_blend_backward_groups(b.tiles_x, b.tiles_y, 4);
+  if (blocks <= 0) return GS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  k_blend_bwd<true, true><<<(unsigned)blocks, kWave, 0, s>>>(
+      b, BwdStats{reinterpret_cast<unsigned long long *>(hist), per_group});
+  return check_launch("gs_blend_backward_lane_stats");
 }
 
 namespace {

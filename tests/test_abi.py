@@ -15,7 +15,7 @@ HDR = os.path.join(ROOT, "include", "gsplat_mi355x.h")
 
 def declared_functions():
     src = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:gs_status|size_t|int32_t|void|const char \*)\s*(gs_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:gs_status|size_t|int32_t|int64_t|void|const char \*)\s*(gs_\w+)\s*\(", src, re.M)))
 
 
 def test_header_and_binding_agree(pkg):
