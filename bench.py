@@ -118,12 +118,12 @@ class BenchCamera:
         return self._wv
 
 
-def algorithmic_counts(fr, pair_counts, H, W, tiles_x, tiles_y):
+def algorithmic_counts(pix_neval, pair_counts, H, W, tiles_x, tiles_y):
     """SURVEY 8(d) work counters of one frame: R (records consumed per tile:
     list prefix up to the deepest pixel's last evaluated entry), E (evaluated
-    pairs) from the forward's saved per-pixel state, C (contributing pairs)
-    from the forward's measurement counter."""
-    neval = fr.pix_state[:, 1].contiguous().view(torch.int32).view(H, W).to(torch.int64)
+    pairs) and C (contributing pairs) from the forward's per-pixel
+    measurement counters."""
+    neval = pix_neval.view(H, W).to(torch.int64)
     E = int(neval.sum())
     pad = torch.zeros(tiles_y * 16, tiles_x * 16, dtype=torch.int64, device=neval.device)
     pad[:H, :W] = neval
@@ -272,10 +272,11 @@ def main():
         from mini3dgs_amd import rasterizer as RZ
         camp = pkg.camera_params(cam, settings)
         pair_counts = torch.empty((H * W,), dtype=torch.int32, device=dev)
+        pix_neval = torch.empty((H * W,), dtype=torch.int32, device=dev)
         _, _, _, _, _, _, _, fr = RZ.forward_pipeline(
             camp, model._xyz, None, model._scaling, model._rotation, model._features_dc[:, 0, :],
-            torch.sigmoid(model._opacity).squeeze(1), pair_counts=pair_counts)
-        R, E, Cc = algorithmic_counts(fr, pair_counts, H, W, tiles_x, tiles_y)
+            torch.sigmoid(model._opacity).squeeze(1), pair_counts=pair_counts, pix_neval=pix_neval)
+        R, E, Cc = algorithmic_counts(pix_neval, pair_counts, H, W, tiles_x, tiles_y)
         M, T = fr.M, fr.T
         num_tiles = tiles_x * tiles_y
         # SURVEY 8(d) algorithmic bytes per launch: the consumed records (44 B:

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 19
+#define GS_ABI_VERSION 20
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 4096      /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
                                  of at least max(W, H) renders the same as any larger one (one tile
@@ -248,8 +248,12 @@ typedef struct gs_blend_fwd_args {
   float *image;                 /* [3,H,W] */
   float *alpha;                 /* [H,W]   */
   float *depth;                 /* [H,W]   */
-  float *pix_acc;               /* [H*W,4] */
-  float *pix_state;             /* [H*W,2] */
+  uint8_t *pix_flags;           /* [H*W] the backward's per-pixel state beside the outputs: bit c
+                                   (c = 0..2) set where channel c's composite left [0, 1] (its clamp
+                                   blocks the gradient), bit 3 likewise for alpha */
+  uint32_t *cell_neval;         /* [num_tiles * gs_tile_quads(tile_size)]: per (tile, 8x8 cell q),
+                                   at tile * cells + q, the entries of the tile's list up to the last
+                                   one any of the cell's pixels evaluated */
   uint64_t *live_bits;          /* [gs_tile_quads(tile_size), live_words]: see gs_blend_live_words;
                                    NULL: none written (a caller's memory budget for large tiles; the
                                    backward then replays every entry of a cell's evaluated prefix) */
@@ -257,6 +261,9 @@ typedef struct gs_blend_fwd_args {
   uint32_t *pair_counts;        /* [H*W] or NULL: each pixel's contributing pairs (c > 0), the
                                    work counter C of SURVEY 8(d); measurement only */
   int32_t num_pairs;            /* T, the entries of sorted_gauss: tile ranges are clamped to it */
+  uint32_t *pix_neval;          /* [H*W] or NULL: each pixel's evaluated entries (the work counter
+                                   E of SURVEY 8(d), and the oracle's decision-forced replay);
+                                   measurement only */
 } gs_blend_fwd_args;
 gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
 
@@ -298,8 +305,11 @@ typedef struct gs_blend_bwd_args {
   const uint32_t *ranges;
   const uint32_t *sorted_gauss;
   const float *records;         /* with pair offsets (gs_bin_emit) */
-  const float *pix_acc;
-  const float *pix_state;
+  const float *image;           /* the forward's outputs, unmodified */
+  const float *alpha;
+  const float *depth;
+  const uint8_t *pix_flags;     /* gs_blend_fwd_args.pix_flags / cell_neval of the same forward */
+  const uint32_t *cell_neval;
   const float *g_image;         /* [3,H,W] dL/dimage */
   const float *g_alpha;         /* [H,W] or NULL */
   const float *g_depth;         /* [H,W] or NULL */
@@ -510,6 +520,7 @@ typedef struct gs_render_fwd_args {
   volatile uint32_t *host_counters_host; /* ... and host address of the same buffer */
   uint32_t host_seq;               /* this frame's sequence word (never the previous frame's) */
   uint32_t *pair_counts;           /* optional, gs_blend_fwd_args.pair_counts */
+  uint32_t *pix_neval;             /* optional, gs_blend_fwd_args.pix_neval */
   int32_t resume;                  /* 1: continue after GS_NEED_CAPACITY, with a tile workspace of >= T */
   /* results (and state for resume / the backward) */
   int32_t M, T;
@@ -527,6 +538,7 @@ typedef struct gs_render_bwd_args {
   int32_t M, T, tile_alt;          /* the forward's results */
   const float *means2d, *conics;   /* the forward's outputs */
   const uint8_t *vis;
+  const float *image, *alpha, *depth; /* the forward's outputs, unmodified (the blend backward reads them) */
   const float *g_image, *g_alpha, *g_depth; /* pixel cotangents (g_image NULL: none) */
   const float *g_means2d, *g_conics;        /* optional */
   float *pair_grads;               /* [T * fb.flag_groups, GS_PARTIAL_STRIDE] scratch */
@@ -542,7 +554,8 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream);
 /* Byte offsets of the buffers inside the two workspaces (for diagnostics and
  * tests that inspect a frame): frame -- records, rects, depth keys [2,n],
  * depth ids [2,n], key_minmax, counters, sort workspace, binning workspace,
- * pair_offset, tile ranges, pix_acc, pix_state, grad_sums, total; tile -- tile
+ * pair_offset, tile ranges, pixel clamp flags, per-cell evaluated entries
+ * (gs_blend_fwd_args.pix_flags / cell_neval), grad_sums, total; tile -- tile
  * keys (two halves), Gaussian ids (two halves), sort workspace, liveness
  * bitmap, slot flags, total, liveness words per cell. */
 void gs_frame_offsets(int32_t n, int32_t width, int32_t height, int32_t tile_size, size_t out[14]);

@@ -27,7 +27,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 19
+GS_ABI_VERSION = 20
 GS_NEED_CAPACITY, GS_RETRY_FULL_KEYS = 4, 5  # gs_render_forward: what to do next (not errors)
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
@@ -81,16 +81,16 @@ class GsBlendFwdArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
         ("sorted_gauss", _vp), ("records", _vp), ("image", _vp), ("alpha", _vp), ("depth", _vp),
-        ("pix_acc", _vp), ("pix_state", _vp), ("live_bits", _vp), ("live_words", C.c_int64),
-        ("pair_counts", _vp), ("num_pairs", C.c_int32),
+        ("pix_flags", _vp), ("cell_neval", _vp), ("live_bits", _vp), ("live_words", C.c_int64),
+        ("pair_counts", _vp), ("num_pairs", C.c_int32), ("pix_neval", _vp),
     ]
 
 
 class GsBlendBwdArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
-        ("sorted_gauss", _vp), ("records", _vp), ("pix_acc", _vp),
-        ("pix_state", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp),
+        ("sorted_gauss", _vp), ("records", _vp), ("image", _vp), ("alpha", _vp), ("depth", _vp),
+        ("pix_flags", _vp), ("cell_neval", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp),
         ("live_bits", _vp), ("live_words", C.c_int64), ("pair_grads", _vp), ("slot_live", _vp),
         ("num_pairs", C.c_int32), ("cell_begin", C.c_int32), ("cell_count", C.c_int32),
     ]
@@ -119,7 +119,7 @@ class GsRenderFwdArgs(C.Structure):
         ("image", _vp), ("alpha", _vp), ("depth", _vp), ("fb", GsFrameBuffers), ("key_base", C.c_uint32),
         ("key_bits", C.c_int32), ("depth_sort_msd", C.c_int32), ("zero_slot_flags", C.c_int32),
         ("host_counters_dev", _vp), ("host_counters_host", _vp), ("host_seq", C.c_uint32), ("pair_counts", _vp),
-        ("resume", C.c_int32), ("M", C.c_int32), ("T", C.c_int32), ("depth_min_bits", C.c_uint32),
+        ("pix_neval", _vp), ("resume", C.c_int32), ("M", C.c_int32), ("T", C.c_int32), ("depth_min_bits", C.c_uint32),
         ("depth_max_bits", C.c_uint32), ("depth_alt", C.c_int32), ("tile_alt", C.c_int32),
     ]
 
@@ -127,8 +127,8 @@ class GsRenderFwdArgs(C.Structure):
 class GsRenderBwdArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("g", GsGaussians), ("fb", GsFrameBuffers), ("M", C.c_int32), ("T", C.c_int32),
-        ("tile_alt", C.c_int32), ("means2d", _vp), ("conics", _vp), ("vis", _vp), ("g_image", _vp),
-        ("g_alpha", _vp), ("g_depth", _vp), ("g_means2d", _vp), ("g_conics", _vp), ("pair_grads", _vp),
+        ("tile_alt", C.c_int32), ("means2d", _vp), ("conics", _vp), ("vis", _vp), ("image", _vp),
+        ("alpha", _vp), ("depth", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp), ("g_means2d", _vp), ("g_conics", _vp), ("pair_grads", _vp),
         ("flags_zeroed", C.c_int32), ("project", C.c_int32), ("d_xyz", _vp), ("d_cov3d", _vp),
         ("d_scaling", _vp), ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
         ("grad_sums", _vp), ("blend_events", _vp * 2),

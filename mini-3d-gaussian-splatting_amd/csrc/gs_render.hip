@@ -23,11 +23,11 @@ size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // frame_ws: per-Gaussian and per-pixel buffers (offsets in bytes)
 struct FrameLayout {
-  size_t records, rects, keys, vals, key_minmax, counters, sort_ws, bin_ws, pair_offset, ranges, pix_acc, pix_state,
-      grad_sums, total;
+  size_t records, rects, keys, vals, key_minmax, counters, sort_ws, bin_ws, pair_offset, ranges, pix_flags,
+      cell_neval, grad_sums, total;
 };
 
-FrameLayout frame_layout(int32_t n, int32_t W, int32_t H, int32_t tiles) {
+FrameLayout frame_layout(int32_t n, int32_t W, int32_t H, int32_t tiles, int32_t cells) {
   FrameLayout L;
   const size_t un = (size_t)(n > 0 ? n : 0), hw = (size_t)W * (size_t)H;
   size_t o = 0;
@@ -46,8 +46,8 @@ FrameLayout frame_layout(int32_t n, int32_t W, int32_t H, int32_t tiles) {
   L.bin_ws = take(gs_bin_workspace_bytes(n > 0 ? n : 1));
   L.pair_offset = take(un * 4);
   L.ranges = take((size_t)tiles * 8);
-  L.pix_acc = take(hw * 16);
-  L.pix_state = take(hw * 8);
+  L.pix_flags = take(hw);
+  L.cell_neval = take((size_t)tiles * (size_t)(cells > 0 ? cells : 0) * 4);
   L.grad_sums = take(un * GS_PAIR_GRAD_FLOATS * 4);
   L.total = o;
   return L;
@@ -82,8 +82,9 @@ TileLayout tile_layout(int64_t cap, int32_t tiles, int32_t live_cells, int32_t f
 
 int32_t div_up_i(int32_t a, int32_t b) { return (a + b - 1) / b; }
 
-bool fb_ok(const gs_frame_buffers &fb, int32_t n, int32_t W, int32_t H, int32_t tiles, size_t *need_frame) {
-  const FrameLayout F = frame_layout(n, W, H, tiles);
+bool fb_ok(const gs_frame_buffers &fb, int32_t n, int32_t W, int32_t H, int32_t tiles, int32_t cells,
+           size_t *need_frame) {
+  const FrameLayout F = frame_layout(n, W, H, tiles, cells);
   *need_frame = F.total;
   return fb.frame_ws && fb.frame_ws_bytes >= F.total;
 }
@@ -104,7 +105,7 @@ extern "C" {
 size_t gs_frame_workspace_bytes(int32_t n, int32_t width, int32_t height, int32_t tile_size) {
   if (n < 0 || width <= 0 || height <= 0 || tile_size < 1) return 0;
   const int32_t tiles = div_up_i(width, tile_size) * div_up_i(height, tile_size);
-  return frame_layout(n, width, height, tiles).total;
+  return frame_layout(n, width, height, tiles, gs_tile_quads(tile_size)).total;
 }
 
 size_t gs_tile_workspace_bytes(int64_t capacity, int32_t num_tiles, int32_t live_cells, int32_t flag_groups) {
@@ -118,13 +119,14 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   const int32_t n = a->g.n, W = a->cam.image_width, H = a->cam.image_height, L = a->cam.tile_size;
   if (n < 0 || W <= 0 || H <= 0 || L < 1) return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: bad sizes", what);
   const int32_t tiles_x = div_up_i(W, L), tiles_y = div_up_i(H, L), tiles = tiles_x * tiles_y;
+  const int32_t cells = gs_tile_quads(L);
   size_t need = 0;
-  if (!fb_ok(a->fb, n, W, H, tiles, &need))
+  if (!fb_ok(a->fb, n, W, H, tiles, cells, &need))
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: frame workspace missing or below gs_frame_workspace_bytes", what);
   if (!a->host_counters_dev || !a->host_counters_host)
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: the pinned counter buffer (device and host address) is required",
                             what);
-  const FrameLayout F = frame_layout(n, W, H, tiles);
+  const FrameLayout F = frame_layout(n, W, H, tiles, cells);
   char *fw = reinterpret_cast<char *>(a->fb.frame_ws);
   float *records = reinterpret_cast<float *>(fw + F.records);
   uint32_t *rects = reinterpret_cast<uint32_t *>(fw + F.rects);
@@ -257,8 +259,9 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   fa.image = a->image;
   fa.alpha = a->alpha;
   fa.depth = a->depth;
-  fa.pix_acc = reinterpret_cast<float *>(fw + F.pix_acc);
-  fa.pix_state = reinterpret_cast<float *>(fw + F.pix_state);
+  fa.pix_flags = reinterpret_cast<uint8_t *>(fw + F.pix_flags);
+  fa.cell_neval = reinterpret_cast<uint32_t *>(fw + F.cell_neval);
+  fa.pix_neval = a->pix_neval;
   fa.live_bits = a->fb.live_cells > 0 ? reinterpret_cast<uint64_t *>(tw + T0.live) : nullptr;
   fa.live_words = (int64_t)T0.live_words;
   fa.pair_counts = a->pair_counts;
@@ -272,18 +275,20 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
   const int32_t n = a->g.n, W = a->cam.image_width, H = a->cam.image_height, L = a->cam.tile_size;
   if (n < 0 || W <= 0 || H <= 0 || L < 1) return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: bad sizes", what);
   const int32_t tiles_x = div_up_i(W, L), tiles_y = div_up_i(H, L), tiles = tiles_x * tiles_y;
+  const int32_t cells = gs_tile_quads(L), G = a->fb.flag_groups;
   size_t need = 0;
-  if (!fb_ok(a->fb, n, W, H, tiles, &need))
+  if (!fb_ok(a->fb, n, W, H, tiles, cells, &need))
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: frame workspace missing or below gs_frame_workspace_bytes", what);
-  const FrameLayout F = frame_layout(n, W, H, tiles);
+  const FrameLayout F = frame_layout(n, W, H, tiles, cells);
   char *fw = reinterpret_cast<char *>(a->fb.frame_ws);
   float *grad_sums = reinterpret_cast<float *>(fw + F.grad_sums);
   a->grad_sums = grad_sums;
   gs_status st;
   const bool pixel_grads = a->M > 0 && a->T > 0 && a->g_image;
-  const int32_t cells = gs_tile_quads(L), G = a->fb.flag_groups;
   if (pixel_grads) {
     if (!a->pair_grads || G < 1) return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: pair_grads / flag_groups", what);
+    if (!a->image || !a->alpha || !a->depth)
+      return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: the forward's image / alpha / depth are required", what);
     const TileLayout T0 = tile_layout(a->fb.capacity, tiles, a->fb.live_cells, G);
     char *tw = reinterpret_cast<char *>(a->fb.tile_ws);
     if (!tw || a->fb.tile_ws_bytes < T0.total)
@@ -297,8 +302,11 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
     b.ranges = reinterpret_cast<const uint32_t *>(fw + F.ranges);
     b.sorted_gauss = reinterpret_cast<const uint32_t *>(tw + (a->tile_alt ? T0.tv[1] : T0.tv[0]));
     b.records = reinterpret_cast<const float *>(fw + F.records);
-    b.pix_acc = reinterpret_cast<const float *>(fw + F.pix_acc);
-    b.pix_state = reinterpret_cast<const float *>(fw + F.pix_state);
+    b.image = a->image;
+    b.alpha = a->alpha;
+    b.depth = a->depth;
+    b.pix_flags = reinterpret_cast<const uint8_t *>(fw + F.pix_flags);
+    b.cell_neval = reinterpret_cast<const uint32_t *>(fw + F.cell_neval);
     b.g_image = a->g_image;
     b.g_alpha = a->g_alpha;
     b.g_depth = a->g_depth;
@@ -374,9 +382,10 @@ void gs_frame_offsets(int32_t n, int32_t width, int32_t height, int32_t tile_siz
   if (!out) return;
   const int32_t tiles = (width > 0 && height > 0 && tile_size > 0)
                             ? div_up_i(width, tile_size) * div_up_i(height, tile_size) : 0;
-  const FrameLayout F = frame_layout(n, width > 0 ? width : 0, height > 0 ? height : 0, tiles);
+  const FrameLayout F = frame_layout(n, width > 0 ? width : 0, height > 0 ? height : 0, tiles,
+                                     tile_size > 0 ? gs_tile_quads(tile_size) : 0);
   const size_t v[14] = {F.records, F.rects,  F.keys,    F.vals,      F.key_minmax, F.counters,  F.sort_ws,
-                        F.bin_ws,  F.pair_offset, F.ranges, F.pix_acc, F.pix_state, F.grad_sums, F.total};
+                        F.bin_ws,  F.pair_offset, F.ranges, F.pix_flags, F.cell_neval, F.grad_sums, F.total};
   memcpy(out, v, sizeof(v));
 }
 

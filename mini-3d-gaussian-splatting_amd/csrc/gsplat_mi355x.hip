@@ -1283,18 +1283,28 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
     const uint64_t wi = (b - start) / 64u;
     if (lane == 0 && wi < live_left) live[wi] = livem;
   }
-  if (!inside) return;
   if ((runm >> lane) & 1ull) neval = last;
-  if (A < kAlphaStop) neval = end - start;
+  if (inside && A < kAlphaStop) neval = end - start;
+  // the cell's last evaluated entry (the backward replays up to it): lanes
+  // outside the tile or image evaluated none
+  const uint32_t cstop = wave_max_u32(inside ? neval : 0u);
+  if (lane == 0) a.cell_neval[(size_t)tile * ncell + quad] = cstop;
+  if (!inside) return;
   const size_t HW = (size_t)W * H, p = (size_t)py * W + px;
   const float tb = 1.f - A;
-  a.image[p] = clamp01(ar + tb * bg0);  // :359,364
-  a.image[HW + p] = clamp01(ag + tb * bg1);
-  a.image[2 * HW + p] = clamp01(ab + tb * bg2);
+  const float pr = ar + tb * bg0, pg = ag + tb * bg1, pb = ab + tb * bg2;  // :359,364
+  a.image[p] = clamp01(pr);
+  a.image[HW + p] = clamp01(pg);
+  a.image[2 * HW + p] = clamp01(pb);
   a.alpha[p] = clamp01(A);
   a.depth[p] = D / (A + 1e-6f);  // :362
-  reinterpret_cast<float4 *>(a.pix_acc)[p] = make_float4(ar, ag, ab, D);
-  reinterpret_cast<float2 *>(a.pix_state)[p] = make_float2(A, __uint_as_float(neval));
+  // The backward's per-pixel state is these outputs plus one byte: which
+  // clamps blocked (value outside [0, 1], NaN included).  An unblocked
+  // channel's image is the composite itself and A never leaves [0, 1] (each
+  // step adds c <= 1 - A, rounded), so alpha is A.
+  a.pix_flags[p] = (uint8_t)((pr >= 0.f && pr <= 1.f ? 0u : 1u) | (pg >= 0.f && pg <= 1.f ? 0u : 2u) |
+                             (pb >= 0.f && pb <= 1.f ? 0u : 4u) | (A >= 0.f && A <= 1.f ? 0u : 8u));
+  if (a.pix_neval) a.pix_neval[p] = neval;
   if constexpr (kCount) a.pair_counts[p] = ncontrib;
 }
 
@@ -1418,8 +1428,11 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
   const uint32_t gid0 = a.sorted_gauss[start + (uint32_t)lane < lend ? start + (uint32_t)lane : 0u];
   const size_t HW = (size_t)W * H;
   const size_t p = inside ? (size_t)py * W + px : 0;
-  const float4 acc = reinterpret_cast<const float4 *>(a.pix_acc)[p];
-  const float2 st = reinterpret_cast<const float2 *>(a.pix_state)[p];
+  // the forward's outputs and clamp flags (k_blend_fwd): alpha is A, an
+  // unblocked channel's image its composite
+  const float im0 = a.image[p], im1 = a.image[HW + p], im2 = a.image[2 * HW + p];
+  const float al = a.alpha[p], dep = a.depth[p];
+  const uint32_t fl = a.pix_flags[p];
   const float gi0 = a.g_image[p], gi1 = a.g_image[HW + p], gi2 = a.g_image[2 * HW + p];
   const float gal = (a.g_alpha ? a.g_alpha : a.g_image)[p];
   const float gdp = (a.g_depth ? a.g_depth : a.g_image)[p];
@@ -1427,23 +1440,25 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
   const float bg0 = a.cam.bg[0], bg1 = a.cam.bg[1], bg2 = a.cam.bg[2];
   // pixel cotangents through clamp / bg composite / depth normalisation
   // (selects, no branch: the compiler would sink the loads into it)
-  const float tr = inside ? acc.x : 0.f, tg = inside ? acc.y : 0.f, tbl = inside ? acc.z : 0.f;
-  const float Dt = inside ? acc.w : 0.f, At = inside ? st.x : 0.f;
-  const uint32_t neval = inside ? __float_as_uint(st.y) : 0u;
+  const float At = inside ? al : 0.f;
   const float tb = 1.f - At;
-  const float pr = tr + tb * bg0, pg = tg + tb * bg1, pb = tbl + tb * bg2;
-  const float gR0 = (inside && pr >= 0.f && pr <= 1.f) ? gi0 : 0.f;
-  const float gR1 = (inside && pg >= 0.f && pg <= 1.f) ? gi1 : 0.f;
-  const float gR2 = (inside && pb >= 0.f && pb <= 1.f) ? gi2 : 0.f;
+  const float gR0 = (inside && !(fl & 1u)) ? gi0 : 0.f;
+  const float gR1 = (inside && !(fl & 2u)) ? gi1 : 0.f;
+  const float gR2 = (inside && !(fl & 4u)) ? gi2 : 0.f;
+  // the accumulated colour without the background, where its gradient passes
+  // (where it is blocked, gR = 0 and the value is not used)
+  const float tr = inside ? im0 - tb * bg0 : 0.f, tg = inside ? im1 - tb * bg1 : 0.f;
+  const float tbl = inside ? im2 - tb * bg2 : 0.f;
+  const float Dt = inside ? dep * (At + 1e-6f) : 0.f;
   float gA = -gR0 * bg0 - gR1 * bg1 - gR2 * bg2;
-  if (inside && a.g_alpha && At >= 0.f && At <= 1.f) gA += gal;
+  if (inside && a.g_alpha && !(fl & 8u)) gA += gal;
   const bool has_d = inside && a.g_depth;
   const float den = At + 1e-6f;
   const float gD = has_d ? gdp / den : 0.f;
   const float gAd = -gdp * Dt / (den * den);
   if (has_d) gA += gAd;
-  // the quadrant's last evaluated entry: nothing past it carries gradient here
-  const uint32_t wstop = __builtin_amdgcn_readfirstlane(wave_max_u32(neval));
+  // the cell's last evaluated entry: nothing past it carries gradient here
+  const uint32_t wstop = __builtin_amdgcn_readfirstlane(a.cell_neval[(size_t)tile * cg.cells() + quad]);
   if (wstop == 0) return;
   s_pg[lane] = make_float4(gR0, gR1, gR2, gD);
   const float fx = (float)px, fy = (float)py;
@@ -2395,7 +2410,7 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_blend_forward");
   if (!tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_forward");
-  if (!a->ranges || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_acc || !a->pix_state ||
+  if (!a->ranges || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_flags || !a->cell_neval ||
       (a->live_bits && a->live_words <= 0) || (a->num_pairs > 0 && !a->sorted_gauss))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_forward");
   if (a->num_pairs < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative num_pairs", "gs_blend_forward");
@@ -2417,7 +2432,8 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   if (!cam_ok(a->cam)) return fail(GS_ERR_UNSUPPORTED, kCamMsg, "gs_blend_backward");
   if (!tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: tiles_x/tiles_y do not match the image", "gs_blend_backward");
-  if (!a->ranges || !a->sorted_gauss || !a->records || !a->pix_acc || !a->pix_state || !a->g_image ||
+  if (!a->ranges || !a->sorted_gauss || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_flags ||
+      !a->cell_neval || !a->g_image ||
       !a->pair_grads || !a->slot_live || (a->live_bits && a->live_words <= 0))
     return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_blend_backward");
   if (a->num_pairs < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative num_pairs", "gs_blend_backward");
@@ -2449,7 +2465,8 @@ gs_status gs_blend_backward_lane_stats(const gs_blend_bwd_args *a, uint64_t *his
   if (!a || !hist || !per_group) return fail(GS_ERR_INVALID_ARG, "%s: null args", "gs_blend_backward_lane_stats");
   if (a->cam.tile_size != GS_DEFAULT_TILE || !(a->cell_begin == 0 && (a->cell_count == 0 || a->cell_count == 4)))
     return fail(GS_ERR_UNSUPPORTED, "%s: the default tile, one batch", "gs_blend_backward_lane_stats");
-  if (!a->ranges || !a->sorted_gauss || !a->records || !a->pix_acc || !a->pix_state || !a->g_image ||
+  if (!a->ranges || !a->sorted_gauss || !a->records || !a->image || !a->alpha || !a->depth || !a->pix_flags ||
+      !a->cell_neval || !a->g_image ||
       !a->pair_grads || !a->slot_live || !tiles_match(a->cam, a->tiles_x, a->tiles_y))
     return fail(GS_ERR_INVALID_ARG, "%s: bad buffers", "gs_blend_backward_lane_stats");
   gs_blend_bwd_args b = *a;

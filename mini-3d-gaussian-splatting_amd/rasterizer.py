@@ -239,8 +239,8 @@ def _check_inputs(xyz: torch.Tensor):
 
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
-    __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_acc",
-                 "pix_state", "live_bits", "big", "M", "T", "slot_live", "groups")
+    __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_flags",
+                 "cell_neval", "live_bits", "big", "M", "T", "slot_live", "groups")
 
 
 _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess)
@@ -468,8 +468,8 @@ class _FastFrame:
     order = property(lambda s: s._f(3, 8 * s.n, torch.int32, (2, s.n))[s.fa.depth_alt])
     pair_offset = property(lambda s: s._f(8, 4 * s.n, torch.int32, (s.n,)))
     ranges = property(lambda s: s._f(9, 8 * s.tiles, torch.int32, (s.tiles, 2)))
-    pix_acc = property(lambda s: s._f(10, 16 * s.HW, torch.float32, (s.HW, 4)))
-    pix_state = property(lambda s: s._f(11, 8 * s.HW, torch.float32, (s.HW, 2)))
+    pix_flags = property(lambda s: s._f(10, s.HW, torch.uint8, (s.HW,)))
+    cell_neval = property(lambda s: s._f(11, 4 * s.tiles * s.cells, torch.int32, (s.tiles, s.cells)))
     sorted_gauss = property(lambda s: s._t(2 + s.fa.tile_alt, 4 * s.T, torch.int32, (s.T,)))
     live_bits = property(lambda s: s._t(5, 8 * s.cells * s._o()[1][8], torch.int64, (s.cells, s._o()[1][8])))
     slot_live = property(lambda s: s._t(6, s.groups * s.T, torch.uint8, (s.groups * s.T,)))
@@ -487,7 +487,7 @@ def _host_counters(dev) -> "_HostCounters":
 
 
 def _forward_frame(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest,
-                   sh_degree, pair_counts, depth_window_ok, need_grad, hc):
+                   sh_degree, pair_counts, depth_window_ok, need_grad, hc, pix_neval):
     """forward_pipeline through gs_render_forward (the default tile)."""
     lib = N.load()
     dev = xyz.device
@@ -534,7 +534,7 @@ def _forward_frame(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opa
     fa.zero_slot_flags = 1 if need_grad else 0
     hc.seq = hc.seq % 0x7FFFFFFF + 1
     fa.host_counters_dev, fa.host_counters_host, fa.host_seq = hc.dptr, hc.t.data_ptr(), hc.seq
-    fa.pair_counts = N.ptr(pair_counts)
+    fa.pair_counts, fa.pix_neval = N.ptr(pair_counts), N.ptr(pix_neval)
     st = lib.gs_render_forward(C.byref(fa), s)
     if st == N.GS_RETRY_FULL_KEYS:
         # a visible depth outside the window, or an MSD bucket over capacity
@@ -544,7 +544,8 @@ def _forward_frame(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opa
             _note_window_miss(dev)
         _T_SEEN[dev] = fa.T
         return forward_pipeline(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit,
-                                sh_rest, sh_degree, pair_counts, depth_window_ok=False, need_grad=need_grad)
+                                sh_rest, sh_degree, pair_counts, depth_window_ok=False, need_grad=need_grad,
+                                pix_neval=pix_neval)
     if st == N.GS_NEED_CAPACITY:
         cap = fa.T
         tws = int(lib.gs_tile_workspace_bytes(cap, tiles, cam.cells, cam.groups))
@@ -571,9 +572,11 @@ def _forward_frame(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opa
 
 
 def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
-                     sh_rest=None, sh_degree=0, pair_counts=None, depth_window_ok=True, need_grad=False):
-    """pair_counts: optional int32 [H*W] the blend fills with each pixel's
-    contributing pairs (a measurement counter; not in render()).
+                     sh_rest=None, sh_degree=0, pair_counts=None, depth_window_ok=True, need_grad=False,
+                     pix_neval=None):
+    """pair_counts / pix_neval: optional int32 [H*W] the blend fills with each
+    pixel's contributing pairs / evaluated entries (measurement counters,
+    SURVEY 8d, and the oracle's decision-forced replay; not in render()).
 
     The depth sort runs over a window of the depth keys' bits chosen from the
     previous frame's visible depth range on this device (one radix pass less
@@ -584,7 +587,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         hc = _host_counters(xyz.device)
         if hc.dptr is not None:
             return _forward_frame(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit, sh_rest,
-                                  sh_degree, pair_counts, depth_window_ok, need_grad, hc)
+                                  sh_degree, pair_counts, depth_window_ok, need_grad, hc, pix_neval)
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -656,8 +659,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
         image = torch.empty((3, H, W), dtype=f32, device=dev)
         alpha = torch.empty((1, H, W), dtype=f32, device=dev)
         depth = torch.empty((1, H, W), dtype=f32, device=dev)
-        pix_acc = torch.empty((H * W, 4), dtype=f32, device=dev)
-        pix_state = torch.empty((H * W, 2), dtype=f32, device=dev)
+        pix_flags = torch.empty((H * W,), dtype=torch.uint8, device=dev)
+        cell_neval = torch.empty((num_tiles, cam.cells), dtype=i32, device=dev)
         # the T-sized buffers too, at a capacity guessed from the last frame on
         # this device, and the emission queued into them before the sync (it
         # drops entries past the capacity): its kernel time hides the
@@ -692,7 +695,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
                 _note_window_miss(dev)
             _T_SEEN[dev] = T
             return forward_pipeline(cam, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit,
-                                    sh_rest, sh_degree, pair_counts, depth_window_ok=False, need_grad=need_grad)
+                                    sh_rest, sh_degree, pair_counts, depth_window_ok=False, need_grad=need_grad,
+                                    pix_neval=pix_neval)
     else:
         M, T = 0, 0
     fr.M, fr.T = M, T
@@ -733,8 +737,8 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     N.check(lib.gs_tile_ranges(C.byref(ra), s), "gs_tile_ranges")
 
     fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), L.p_tv[alt.value], N.ptr(records),
-                          N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_acc), N.ptr(pix_state),
-                          L.p_live, L.live_words, N.ptr(pair_counts), T)
+                          N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_flags), N.ptr(cell_neval),
+                          L.p_live, L.live_words, N.ptr(pair_counts), T, N.ptr(pix_neval))
     StageTimer.mark("blend_fwd")
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
     StageTimer.mark("~end_fwd")
@@ -750,14 +754,16 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     fr.groups = L.groups
     fr.slot_live = L.big[L.o_flags:L.o_flags + L.groups * T] if need_grad else None
     fr.pair_offset, fr.ranges = pair_offset, ranges
-    fr.pix_acc, fr.pix_state = pix_acc, pix_state
+    fr.pix_flags, fr.cell_neval = pix_flags, cell_neval
     return image, alpha, depth, means2d, conics, radii, vis, fr
 
 
 def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotation, logits, opacity,
                       means2d, conics, g_image, g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit=False,
-                      sh_rest=None, sh_degree=0, out=None):
-    """out: optional preallocated gradient tensors {name: tensor} (the
+                      sh_rest=None, sh_degree=0, out=None, outputs=None):
+    """outputs: the forward's (image, alpha, depth), unmodified -- with the
+    frame's clamp flags they are the blend backward's per-pixel state.
+    out: optional preallocated gradient tensors {name: tensor} (the
     data-parallel bucket's views, distributed.GradAllReduce.attach); the
     kernels write there instead of into fresh buffers.  out["_rows_ready"]
     (optional): called with (lo, hi) once the gradient rows of Gaussians
@@ -765,7 +771,8 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     that a range's all-reduce overlaps the next range's kernels."""
     if isinstance(fr, _FastFrame):
         return _backward_frame(cam, fr, xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics, g_image,
-                               g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit, sh_rest, sh_degree, out)
+                               g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit, sh_rest, sh_degree, out,
+                               outputs)
     lib = N.load()
     dev = xyz.device
     n = int(xyz.shape[0])
@@ -780,6 +787,7 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         g_image = g_image.contiguous()
         g_alpha = None if g_alpha is None else g_alpha.contiguous()
         g_depth = None if g_depth is None else g_depth.contiguous()
+        image, alpha, depth = _blend_outputs(outputs)
         # one partial per (slot, cell of the batch) -- per slot at the default
         # tile, whose cells are combined on chip; only replayed entries write
         # theirs and set its flag.  Other tiles' cells run in batches of
@@ -791,8 +799,8 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         if slot_live is None:
             slot_live = torch.zeros((fr.T * G,), dtype=torch.uint8, device=dev)
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
-                              N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
-                              N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
+                              N.ptr(fr.records), N.ptr(image), N.ptr(alpha), N.ptr(depth),
+                              N.ptr(fr.pix_flags), N.ptr(fr.cell_neval), N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
                               0 if fr.live_bits is None else fr.live_bits.shape[1], N.ptr(pair_grads),
                               N.ptr(slot_live), fr.T, 0, 0)
         if G < cam.groups:
@@ -850,8 +858,21 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
     return d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh
 
 
+def _blend_outputs(outputs):
+    """The forward's image, alpha, depth as the blend backward reads them
+    (fp32, contiguous, as rasterize returned them)."""
+    if outputs is None:
+        raise ValueError("the blend backward needs the forward's (image, alpha, depth)")
+    image, alpha, depth = outputs
+    for t in (image, alpha, depth):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("the forward's image / alpha / depth must be the contiguous fp32 tensors it returned")
+    return image, alpha, depth
+
+
 def _backward_frame(cam: CameraParams, fr: _FastFrame, xyz, cov3d, scaling, rotation, logits, opacity, means2d,
-                    conics, g_image, g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit, sh_rest, sh_degree, out):
+                    conics, g_image, g_alpha, g_depth, g_means2d, g_conics, opacity_is_logit, sh_rest, sh_degree, out,
+                    outputs):
     """backward_pipeline through gs_render_backward (the frame of
     _forward_frame): the blend backward and the gather in the library, then
     the projection backward -- there too unless the data-parallel reduction
@@ -875,6 +896,8 @@ def _backward_frame(cam: CameraParams, fr: _FastFrame, xyz, cov3d, scaling, rota
         g_alpha = None if g_alpha is None else g_alpha.contiguous()
         g_depth = None if g_depth is None else g_depth.contiguous()
         pair_grads = torch.empty((fr.T * fr.groups, N.GS_PARTIAL_STRIDE), dtype=f32, device=dev)
+        image, alpha, depth = _blend_outputs(outputs)
+        ba.image, ba.alpha, ba.depth = image.data_ptr(), alpha.data_ptr(), depth.data_ptr()
         ba.g_image, ba.g_alpha, ba.g_depth = N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth)
         ba.pair_grads = pair_grads.data_ptr()
         ba.flags_zeroed = 1 if fr.slot_live_zeroed else 0
@@ -961,20 +984,23 @@ class RasterizeGaussians(torch.autograd.Function):
             need_grad=_FUSE_FLAGS and any(ctx.needs_input_grad[:7]))
         ctx.cam, ctx.frame, ctx.opacity_is_logit, ctx.sh_degree = cam, fr, opacity_is_logit, sh_degree
         ctx.grad_dest = grad_dest
-        ctx.save_for_backward(xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics)
+        # (the outputs image / alpha / depth too: the blend backward's per-pixel
+        # state; autograd refuses the backward if they were modified in place)
+        ctx.save_for_backward(xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics, image, alpha,
+                              depth)
         ctx.mark_non_differentiable(radii, vis)
         ctx.set_materialize_grads(False)
         return image, alpha, depth, means2d, conics, radii, vis
 
     @staticmethod
     def backward(ctx, g_image, g_alpha, g_depth, g_means2d, g_conics, _g_radii, _g_vis):
-        xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics = ctx.saved_tensors
+        xyz, cov3d, scaling, rotation, logits, opacity, sh_rest, means2d, conics, image, alpha, depth = ctx.saved_tensors
         g_conics = None if g_conics is None else g_conics.reshape(-1, 4)
         dest = ctx.grad_dest() if ctx.grad_dest is not None else None
         d_xyz, d_cov, d_scl, d_rot, d_col, d_op, d_sh = backward_pipeline(
             ctx.cam, ctx.frame, xyz, cov3d, scaling, rotation, logits, opacity, means2d, conics,
             g_image, None if g_alpha is None else g_alpha, g_depth, g_means2d, g_conics, ctx.opacity_is_logit,
-            sh_rest, ctx.sh_degree, out=dest)
+            sh_rest, ctx.sh_degree, out=dest, outputs=(image, alpha, depth))
         need = ctx.needs_input_grad
         return (d_xyz if need[0] else None,
                 d_cov if (cov3d is not None and need[1]) else None,

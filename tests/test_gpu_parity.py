@@ -430,11 +430,11 @@ def test_blend_ranges_clamped_to_entries(pkg, cuda):
     for ranges, want in ((fr.ranges, image), (bad, None)):
         img = torch.full_like(image, -1.0)
         al, dp = torch.empty_like(alpha), torch.empty_like(depth)
-        acc, st = torch.empty_like(fr.pix_acc), torch.empty_like(fr.pix_state)
+        flags, cneval = torch.empty_like(fr.pix_flags), torch.empty_like(fr.cell_neval)
         live = torch.empty_like(fr.live_bits)
         fa = N.GsBlendFwdArgs(cam.to_struct(), cam.tiles_x, cam.tiles_y, N.ptr(ranges), N.ptr(fr.sorted_gauss),
-                              N.ptr(fr.records), N.ptr(img), N.ptr(al), N.ptr(dp), N.ptr(acc), N.ptr(st),
-                              N.ptr(live), live.shape[1], None, T)
+                              N.ptr(fr.records), N.ptr(img), N.ptr(al), N.ptr(dp), N.ptr(flags), N.ptr(cneval),
+                              N.ptr(live), live.shape[1], None, T, None)
         N.check(lib.gs_blend_forward(C.byref(fa), stream), "gs_blend_forward")
         torch.cuda.synchronize()
         assert bool(torch.isfinite(img).all()) and float(img.min()) >= 0.0
@@ -560,7 +560,7 @@ def test_frame_entry_points_data_parallel_ranges(pkg, cuda):
         out = {"_rows_ready": lambda lo, hi: seen.append((lo, hi)), "_chunks": chunks}
         g = torch.ones_like(img)
         d = RZ.backward_pipeline(cam, fr, *[None if t is None else t.detach() for t in raw], m2, cn, g, None, None,
-                                 None, None, opacity_is_logit=True, out=out)
+                                 None, None, opacity_is_logit=True, out=out, outputs=(img, al, dp))
         assert seen == [(20000 * k // chunks, 20000 * (k + 1) // chunks) for k in range(chunks)]
         got.append([t.clone() for t in d if t is not None])
     for a, b in zip(*got):
@@ -715,10 +715,11 @@ def _scene_vs_oracle(pkg, cuda, sc, W, H, bg, seed=1, renderer_kw=None, knife=Tr
         RZ = pkg.rasterizer
         camp = pkg.camera_params(Cam(W, H, sc.fovx, sc.fovy, wv=wv), pkg.RenderSettings(H, W, torch.tensor(bg)),
                                  **{k: kw[k] for k in ("radius_min", "radius_max", "tile_size") if k in kw})
+        pix_neval = torch.empty((H * W,), dtype=torch.int32, device=cuda)
         with torch.no_grad():
-            fr = RZ.forward_pipeline(camp, m._xyz, None, m._scaling, m._rotation, m._features_dc[:, 0, :],
-                                     torch.sigmoid(m._opacity).squeeze(1))[-1]
-        neval = fr.pix_state[:, 1].contiguous().view(torch.int32).view(H, W).cpu().numpy()
+            RZ.forward_pipeline(camp, m._xyz, None, m._scaling, m._rotation, m._features_dc[:, 0, :],
+                                torch.sigmoid(m._opacity).squeeze(1), pix_neval=pix_neval)
+        neval = pix_neval.view(H, W).cpu().numpy()
         osc.force_neval = neval
         reff = G.oracle().render_backward(osc, gi, ga, gd, nthreads=min(16, os.cpu_count() or 1))
         badf = G.pixel_errors(o, reff)

@@ -21,10 +21,12 @@ def main(out):
     m = pkg.synthetic.to_model(sc, pkg.GaussianModel, dev)
     camp = pkg.camera_params(Cam(W, H, sc.fovx, sc.fovy), pkg.RenderSettings(H, W, torch.zeros(3)))
     with torch.no_grad():
+        pn = torch.empty((camp.image_width * camp.image_height,), dtype=torch.int32, device=m._xyz.device)
         image, alpha, depth, *_, fr = RZ.forward_pipeline(camp, m._xyz, None, m._scaling, m._rotation,
-                                                          m._features_dc[:, 0, :], torch.sigmoid(m._opacity).squeeze(1))
+                                                          m._features_dc[:, 0, :], torch.sigmoid(m._opacity).squeeze(1),
+                                                          pix_neval=pn)
     np.savez(out, image=image.cpu().numpy(), alpha=alpha.cpu().numpy(),
-             pix_state=fr.pix_state.cpu().numpy(), ranges=fr.ranges.cpu().numpy())
+             neval=pn.cpu().numpy(), ranges=fr.ranges.cpu().numpy())
 
 
 if __name__ == "__main__":

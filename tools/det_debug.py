@@ -44,7 +44,7 @@ def main():
             torch.cuda.synchronize()
             fr = fr_holder["fr"]
             runs.append(dict(xyz=m._xyz.grad.clone(), op=m._opacity.grad.clone(),
-                             pix=fr.pix_state.clone(), T=fr.T, groups=fr.groups))
+                             pix=fr.pix_flags.int(), T=fr.T, groups=fr.groups))
         for k in ("xyz", "op", "pix"):
             same = [torch.equal(runs[0][k], r[k]) for r in runs[1:]]
             diff = [float((runs[0][k] - r[k]).abs().max()) for r in runs[1:]]

@@ -54,6 +54,7 @@ def run(config="C3", seed=0):
         pair_counts = torch.zeros((H * W,), dtype=torch.int32, device=dev)
         out = RZ.forward_pipeline(camp, m._xyz, None, m._scaling, m._rotation, m._features_dc, m._opacity,
                                   opacity_is_logit=True, pair_counts=pair_counts, need_grad=True)
+    image, alpha, depth = out[:3]
     finally:
         RZ._FRAME_CALLS = saved
     fr = out[7]
@@ -62,8 +63,8 @@ def run(config="C3", seed=0):
 
     def args(pg, sl):
         return N.GsBlendBwdArgs(camp.to_struct(), camp.tiles_x, camp.tiles_y, N.ptr(fr.ranges),
-                                N.ptr(fr.sorted_gauss), N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state),
-                                N.ptr(gi), N.ptr(ga), N.ptr(gd), N.ptr(live), 0 if live is None else live.shape[1],
+                                N.ptr(fr.sorted_gauss), N.ptr(fr.records), N.ptr(image), N.ptr(alpha), N.ptr(depth),
+                                N.ptr(fr.pix_flags), N.ptr(fr.cell_neval), N.ptr(gi), N.ptr(ga), N.ptr(gd), N.ptr(live), 0 if live is None else live.shape[1],
                                 N.ptr(pg), N.ptr(sl), T, 0, 0)
     s = N.stream_ptr()
     pg0 = torch.zeros((T * G, N.GS_PARTIAL_STRIDE), dtype=torch.float32, device=dev)

@@ -32,14 +32,15 @@ def main():
     m = pkg.synthetic.to_model(sc, pkg.GaussianModel, dev)
     camp = pkg.camera_params(Cam(W, H, sc.fovx, sc.fovy), pkg.RenderSettings(H, W, torch.zeros(3)))
     pc = torch.empty((H * W,), dtype=torch.int32, device=dev)
+    pn = torch.empty_like(pc)
     with torch.no_grad():
         for _ in range(2):  # (the second frame takes the depth-key window path, as the bench's)
             image, alpha, depth, *_, fr = RZ.forward_pipeline(
                 camp, m._xyz, None, m._scaling, m._rotation, m._features_dc[:, 0, :],
-                torch.sigmoid(m._opacity).squeeze(1), pair_counts=pc, need_grad=True)
+                torch.sigmoid(m._opacity).squeeze(1), pair_counts=pc, need_grad=True, pix_neval=pn)
     torch.cuda.synchronize()
     np.savez_compressed(a.out, live_bits=fr.live_bits.cpu().numpy(), ranges=fr.ranges.cpu().numpy(),
-                        neval=fr.pix_state[:, 1].contiguous().view(torch.int32).cpu().numpy(),
+                        neval=pn.cpu().numpy(),
                         contrib=pc.cpu().numpy(), W=W, H=H, T=fr.T, M=fr.M)
     print("saved", a.out, "T", fr.T, "live words", fr.live_bits.shape)
 

@@ -39,7 +39,8 @@ def main():
     g = torch.Generator().manual_seed(1)
     gi = (torch.rand((3, H, W), generator=g) * 2 - 1).to(dev)
     ba = N.GsBlendBwdArgs(cam.to_struct(), cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
-                          N.ptr(fr.records), N.ptr(fr.pix_acc), N.ptr(fr.pix_state), N.ptr(gi), 0, 0,
+                          N.ptr(fr.records), N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(fr.pix_flags),
+                          N.ptr(fr.cell_neval), N.ptr(gi), 0, 0,
                           N.ptr(fr.live_bits), fr.live_bits.shape[1], N.ptr(pair_grads), N.ptr(slot_live), fr.T, 0, 0)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()

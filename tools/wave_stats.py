@@ -43,11 +43,13 @@ def main():
     settings = pkg.RenderSettings(image_height=H, image_width=W, bg_color=torch.zeros(3))
     camp = pkg.camera_params(Cam(), settings)
     with torch.no_grad():
+        pn = torch.empty((H * W,), dtype=torch.int32, device=dev)
         *_, fr = RZ.forward_pipeline(camp, model._xyz, None, model._scaling, model._rotation,
-                                     model._features_dc[:, 0, :], torch.sigmoid(model._opacity).squeeze(1))
+                                     model._features_dc[:, 0, :], torch.sigmoid(model._opacity).squeeze(1),
+                                     pix_neval=pn)
     tx_n, ty_n = camp.tiles_x, camp.tiles_y
     ranges = fr.ranges.view(-1, 2).long().cpu()
-    neval = fr.pix_state[:, 1].contiguous().view(torch.int32).view(H, W).long()
+    neval = pn.view(H, W).long()
     pad = torch.zeros(ty_n * 16, tx_n * 16, dtype=torch.long, device=dev)
     pad[:H, :W] = neval
     # per (tile, quadrant) deepest lane
