@@ -54,9 +54,9 @@ def run(config="C3", seed=0):
         pair_counts = torch.zeros((H * W,), dtype=torch.int32, device=dev)
         out = RZ.forward_pipeline(camp, m._xyz, None, m._scaling, m._rotation, m._features_dc, m._opacity,
                                   opacity_is_logit=True, pair_counts=pair_counts, need_grad=True)
-    image, alpha, depth = out[:3]
     finally:
         RZ._FRAME_CALLS = saved
+    image, alpha, depth = out[:3]
     fr = out[7]
     T, G = fr.T, fr.groups
     live = fr.live_bits
