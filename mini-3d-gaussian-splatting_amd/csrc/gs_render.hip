@@ -17,6 +17,10 @@
 #include "gs_internal.h"
 #include "gsplat_mi355x.h"
 
+#ifndef GS_EMIT_TILE_HIST
+#define GS_EMIT_TILE_HIST 0
+#endif
+
 namespace {
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -189,12 +193,15 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   ba.capacity = a->fb.capacity;
   ba.tile_keys = a->fb.capacity > 0 ? reinterpret_cast<uint32_t *>(tw + T0.tk[0]) : nullptr;
   ba.pair_gauss = a->fb.capacity > 0 ? reinterpret_cast<uint32_t *>(tw + T0.tv[0]) : nullptr;
-  // the tile sort's first-pass digit counts come from the emission (the
-  // count clears their table in the tile sort's workspace): one histogram
-  // kernel less
+  // GS_EMIT_TILE_HIST=1 (a variant, off): the tile sort's first-pass digit
+  // counts come from the emission (the count clears their table in the tile
+  // sort's workspace), one histogram kernel less.  Measured at C3: the
+  // emission took 23 -> 36 us against the 5.7 us histogram kernel it saves
+  // (DESIGN.md section 4), so the product keeps the separate histogram.
   const int32_t bits = tiles > 1 ? 32 - __builtin_clz((uint32_t)(tiles - 1)) : 1;
   const int32_t bits0 = gs_internal_first_pass_bits(0, bits);
-  uint32_t *tile_counts = a->fb.capacity > 0 ? reinterpret_cast<uint32_t *>(tw + T0.sort_ws) : nullptr;
+  uint32_t *tile_counts =
+      (GS_EMIT_TILE_HIST && a->fb.capacity > 0) ? reinterpret_cast<uint32_t *>(tw + T0.sort_ws) : nullptr;
   if (!a->resume) {
     // the counts, then -- with a capacity guess -- the emission, queued before
     // the host reads (M, T) back: its kernel time hides the read-back
@@ -203,7 +210,9 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
     volatile uint32_t *hc = a->host_counters_host;
     hc[4] = 0u;  // (the previous frame's sequence word)
     if ((st = gs_internal_bin_count_hist(&ba, tile_counts, bits0, stream))) return st;
-    if (a->fb.capacity > 0 && (st = gs_internal_bin_emit_hist(&ba, tile_counts, bits0, stream))) return st;
+    if (a->fb.capacity > 0 &&
+        (st = tile_counts ? gs_internal_bin_emit_hist(&ba, tile_counts, bits0, stream) : gs_bin_emit(&ba, stream)))
+      return st;
     // the one host synchronisation of a frame: poll the sequence word the
     // count writes through the pinned buffer's device address (no event, no copy)
     const auto t0 = std::chrono::steady_clock::now();
@@ -226,17 +235,21 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   } else {
     if ((int64_t)a->T > a->fb.capacity)
       return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: resume needs a capacity of at least T", what);
-    const size_t words = ((size_t)1 << bits0) * (((size_t)a->fb.capacity + kSortBlockEntries - 1) / kSortBlockEntries);
-    if (hipMemsetAsync(tile_counts, 0, 4 * words, (hipStream_t)stream) != hipSuccess)
-      return gs_internal_fail(GS_ERR_LAUNCH, "%s: count table memset failed", what);
-    if ((st = gs_internal_bin_emit_hist(&ba, tile_counts, bits0, stream))) return st;
+    if (tile_counts) {
+      const size_t words = ((size_t)1 << bits0) * (((size_t)a->fb.capacity + kSortBlockEntries - 1) / kSortBlockEntries);
+      if (hipMemsetAsync(tile_counts, 0, 4 * words, (hipStream_t)stream) != hipSuccess)
+        return gs_internal_fail(GS_ERR_LAUNCH, "%s: count table memset failed", what);
+    }
+    if ((st = tile_counts ? gs_internal_bin_emit_hist(&ba, tile_counts, bits0, stream) : gs_bin_emit(&ba, stream)))
+      return st;
   }
   const int32_t T = a->T;
   int32_t talt = 0;
   uint32_t *tk = reinterpret_cast<uint32_t *>(tw + T0.tk[0]), *tk1 = reinterpret_cast<uint32_t *>(tw + T0.tk[1]);
   uint32_t *tv = reinterpret_cast<uint32_t *>(tw + T0.tv[0]), *tv1 = reinterpret_cast<uint32_t *>(tw + T0.tv[1]);
   if ((st = gs_internal_radix_sort_pairs(tk, tv, tk1, tv1, T, 0, bits, 0, tw + T0.sort_ws,
-                                         gs_radix_sort_workspace_bytes((int32_t)a->fb.capacity), &talt, 1, stream)))
+                                         gs_radix_sort_workspace_bytes((int32_t)a->fb.capacity), &talt,
+                                         GS_EMIT_TILE_HIST ? 1 : 0, stream)))
     return st;
   a->tile_alt = talt;
   gs_range_args ra;

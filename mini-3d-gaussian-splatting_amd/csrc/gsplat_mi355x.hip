@@ -930,7 +930,10 @@ constexpr uint32_t kOwnerCap = kBlock * 64;
 // sort blocks a binning block's output may span with its digit counts in LDS
 // (a block emits ~4.5 K entries at C3, ~3 sort blocks); counts past them go
 // straight to the table
-constexpr int kHistSpan = 8;
+#ifndef GS_HIST_SPAN
+#define GS_HIST_SPAN 8
+#endif
+constexpr int kHistSpan = GS_HIST_SPAN;
 __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials, TileHist th) {
   __shared__ uint32_t s_off[kBlock + 1];
   __shared__ uint32_t s_g[kBlock];
