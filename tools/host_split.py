@@ -84,6 +84,21 @@ def main():
     acc = defaultdict(float)
     proxy = _Timed(lib, acc)
     N.load = lambda: proxy
+    # the rasterizer's own Python around the library calls (the rest of
+    # "render" / "backward" is torch: autograd Function dispatch, the engine)
+    RZ = pkg.rasterizer
+    for fn in ("forward_pipeline", "backward_pipeline", "rasterize"):
+        raw = getattr(RZ, fn)
+
+        def timed(*a, _raw=raw, _n=fn, **k):
+            t0 = time.perf_counter()
+            try:
+                return _raw(*a, **k)
+            finally:
+                parts["py " + _n] += time.perf_counter() - t0
+        setattr(RZ, fn, timed)
+    import importlib
+    importlib.import_module(pkg.__name__ + ".renderer").rasterize = RZ.rasterize
     parts.clear()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
