@@ -12,7 +12,7 @@ and writes, with the result kept out of the rendered model), so that every
 timed frame renders the same scene.  Rank r renders view r of the same replicated 1M
 Gaussian model (weak scaling: one 1080p view per GPU per step).  Inputs are
 resident in HBM before the timed region.  Before the W warm-up steps,
---spinup-steps (default 50, reported in the line) untimed steps bring the GPU
+--spinup-steps (default 50 at C3, more for the small presets; reported in the line) untimed steps bring the GPU
 to its steady clock.  `value` = all ranks' pixels /
 max-over-ranks step time.
 
@@ -52,6 +52,11 @@ REF_BWD_S_PER_CONTRIB_PX = 155e-3 / (256 * 256)
 # SURVEY 8(d) synthetic distribution, and a 4K frame; C3 is the metric's config
 CONFIGS = {"C1": (5_000, 256, 256), "C2": (100_000, 800, 800), "C3": (1_000_000, 1920, 1080),
            "4K": (4_000_000, 3840, 2160)}
+# Untimed spin-up steps per preset, for the GPU clock's ramp over the first
+# ~60 ms of load (profiles/r02/warmup.log): 50 C3 steps are ~60 ms, 50 C1
+# steps only ~15 ms.  (C1 is host-bound; its step time varies 0.21-0.39 ms
+# between runs on the same box whatever the spin-up, profiles/r05/host/.)
+SPINUP_STEPS = {"C1": 1000, "C2": 300, "C3": 50, "4K": 20}
 
 
 def parse():
@@ -71,8 +76,9 @@ def parse():
     # A fixed count (not a time) so that every rank runs the same collectives.
     ap.add_argument("--view", type=int, default=None,
                     help="render rank R's view (diagnostics; default: this rank's own)")
-    ap.add_argument("--spinup-steps", type=int, default=50,
-                    help="untimed steps before the --warmup steps, for the GPU clock ramp")
+    ap.add_argument("--spinup-steps", type=int, default=None,
+                    help="untimed steps before the --warmup steps, for the GPU (and host CPU) clock ramp; "
+                         "default ~60 ms or more of steps: 50 at C3, more for the smaller presets")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="an extra oracle thread count for the CPU sweep (16..256 and the CPU limit always run)")
@@ -85,6 +91,8 @@ def parse():
     a.gaussians = n0 if a.gaussians is None else a.gaussians
     a.width = w0 if a.width is None else a.width
     a.height = h0 if a.height is None else a.height
+    if a.spinup_steps is None:
+        a.spinup_steps = SPINUP_STEPS.get(a.config, 50)
     return a
 
 

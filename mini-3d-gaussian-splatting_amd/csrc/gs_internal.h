@@ -29,3 +29,11 @@ __attribute__((visibility("hidden"))) gs_status gs_internal_bin_count_hist(const
 __attribute__((visibility("hidden"))) gs_status gs_internal_bin_emit_hist(const gs_bin_args *a,
                                                                          uint32_t *tile_counts, int32_t bits,
                                                                          gs_stream_t stream);
+// A stable sort of n <= gs_internal_small_sort_max() (key, value) pairs by the
+// keys' low `bits` bits in one workgroup (LDS passes): keys / vals in
+// (vals NULL: the input positions), keys_out / vals_out out -- the result of
+// gs_radix_sort_pairs over bits [0, bits) in one launch.
+__attribute__((visibility("hidden"))) int32_t gs_internal_small_sort_max(void);
+__attribute__((visibility("hidden"))) gs_status gs_internal_small_sort(const uint32_t *keys, const uint32_t *vals,
+                                                                      uint32_t *keys_out, uint32_t *vals_out,
+                                                                      int32_t n, int32_t bits, gs_stream_t stream);

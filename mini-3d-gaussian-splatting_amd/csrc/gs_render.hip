@@ -175,7 +175,12 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
     if ((st = gs_project_forward(&pa, stream))) return st;
     if (n == 0) return GS_OK;
     int32_t alt = 0;
-    if (a->depth_sort_msd && a->key_bits >= 9 && a->key_bits <= 31)
+    // a frame whose keys fit one workgroup sorts them there in one launch
+    // (the same stable order as the radix passes it replaces)
+    if (n <= gs_internal_small_sort_max()) {
+      st = gs_internal_small_sort(keys, nullptr, keys + un, vals + un, n, a->key_bits, stream);
+      alt = 1;
+    } else if (a->depth_sort_msd && a->key_bits >= 9 && a->key_bits <= 31)
       st = gs_depth_sort_msd(keys, vals, keys + un, vals + un, n, a->key_bits, fw + F.sort_ws,
                              gs_radix_sort_workspace_bytes(n), key_minmax + 1, &alt, stream);
     else
@@ -247,10 +252,14 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   int32_t talt = 0;
   uint32_t *tk = reinterpret_cast<uint32_t *>(tw + T0.tk[0]), *tk1 = reinterpret_cast<uint32_t *>(tw + T0.tk[1]);
   uint32_t *tv = reinterpret_cast<uint32_t *>(tw + T0.tv[0]), *tv1 = reinterpret_cast<uint32_t *>(tw + T0.tv[1]);
-  if ((st = gs_internal_radix_sort_pairs(tk, tv, tk1, tv1, T, 0, bits, 0, tw + T0.sort_ws,
-                                         gs_radix_sort_workspace_bytes((int32_t)a->fb.capacity), &talt,
-                                         GS_EMIT_TILE_HIST ? 1 : 0, stream)))
+  if (T <= gs_internal_small_sort_max() && !tile_counts) {
+    if ((st = gs_internal_small_sort(tk, tv, tk1, tv1, T, bits, stream))) return st;
+    talt = 1;
+  } else if ((st = gs_internal_radix_sort_pairs(tk, tv, tk1, tv1, T, 0, bits, 0, tw + T0.sort_ws,
+                                                gs_radix_sort_workspace_bytes((int32_t)a->fb.capacity), &talt,
+                                                GS_EMIT_TILE_HIST ? 1 : 0, stream))) {
     return st;
+  }
   a->tile_alt = talt;
   gs_range_args ra;
   memset(&ra, 0, sizeof(ra));

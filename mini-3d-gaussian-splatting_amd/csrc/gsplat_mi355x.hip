@@ -601,10 +601,18 @@ constexpr int kMsdWaves = kMsdThreads / kWave;
 constexpr int kMsdIpt = 16;
 constexpr int kMsdCap = kMsdThreads * kMsdIpt;  // 16384 items: 128 KB of keys + values in LDS
 
+// kWhole (gs_internal_small_sort): one workgroup sorts a whole array of
+// n <= kMsdCap keys by their low `lowbits` bits -- the bucket is everything,
+// read from keys / vals (vals NULL: the input positions) and written to
+// keys_out / vals_out.  One launch instead of a radix sort's 3 per pass, for
+// the small frames whose steps are bound by launches.
+template <bool kWhole = false>
 __global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__restrict__ keys,
                                                                uint32_t *__restrict__ vals,
                                                                const uint32_t *__restrict__ totals, int lowbits,
-                                                               uint32_t *overflow) {
+                                                               uint32_t *overflow, uint32_t whole_n = 0u,
+                                                               uint32_t *__restrict__ keys_out = nullptr,
+                                                               uint32_t *__restrict__ vals_out = nullptr) {
   __shared__ uint32_t s_k[kMsdCap], s_v[kMsdCap];
   __shared__ uint32_t wcnt[kMsdWaves][kRadix];
   __shared__ uint32_t s_lbase[kRadix];
@@ -612,7 +620,12 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__res
   __shared__ uint32_t s_seg[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t d0 = blockIdx.x;  // the bucket (grid: 255; bucket 255 is never sorted)
-  if (wave == 0) {
+  if (kWhole) {
+    if (threadIdx.x == 0) {
+      s_seg[0] = 0u;
+      s_seg[1] = whole_n;
+    }
+  } else if (wave == 0) {
     // start = totals[0 .. d0) summed, size = totals[d0]
     uint32_t s = 0;
 #pragma unroll
@@ -629,7 +642,17 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__res
   }
   __syncthreads();
   const uint32_t start = s_seg[0], size = s_seg[1];
-  if (size <= 1u) return;
+  if constexpr (kWhole) {
+    if (size <= 1u) {
+      if (threadIdx.x == 0 && size == 1u) {
+        keys_out[0] = keys[0];
+        vals_out[0] = vals ? vals[0] : 0u;
+      }
+      return;
+    }
+  } else if (size <= 1u) {
+    return;
+  }
   if (size > (uint32_t)kMsdCap) {
     if (threadIdx.x == 0) *overflow = 0xFFFFFFFFu;
     return;
@@ -645,7 +668,7 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__res
     const uint32_t i = (uint32_t)wave * seg + (uint32_t)(r * kWave + lane);
     const uint32_t ic = (r < rounds && i < size) ? i : 0u;
     k_[r] = keys[start + ic];
-    v_[r] = vals[start + ic];
+    v_[r] = (kWhole && !vals) ? ic : vals[start + ic];
   }
   const int passes = (lowbits + kRadixBits - 1) / kRadixBits;
   int shift = 0;
@@ -716,9 +739,10 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__res
       }
     }
   }
+  uint32_t *ko = kWhole ? keys_out : keys, *vo = kWhole ? vals_out : vals;
   for (uint32_t i = threadIdx.x; i < size; i += kMsdThreads) {
-    keys[start + i] = s_k[i];
-    vals[start + i] = s_v[i];
+    ko[start + i] = s_k[i];
+    vo[start + i] = s_v[i];
   }
 }
 
@@ -2294,6 +2318,19 @@ gs_status gs_internal_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t 
   return GS_OK;
 }
 
+int32_t gs_internal_small_sort_max(void) { return kMsdCap; }
+
+gs_status gs_internal_small_sort(const uint32_t *keys, const uint32_t *vals, uint32_t *keys_out, uint32_t *vals_out,
+                                 int32_t n, int32_t bits, gs_stream_t stream) {
+  if (n < 0 || n > kMsdCap || bits < 1 || bits > 32 || (n > 0 && (!keys || !keys_out || !vals_out)))
+    return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_internal_small_sort");
+  if (n == 0) return GS_OK;
+  k_msd_bucket_sort<true><<<1, kMsdThreads, 0, (hipStream_t)stream>>>(
+      const_cast<uint32_t *>(keys), const_cast<uint32_t *>(vals), nullptr, bits, nullptr, (uint32_t)n, keys_out,
+      vals_out);
+  return check_launch("gs_internal_small_sort");
+}
+
 int32_t gs_internal_first_pass_bits(int32_t begin_bit, int32_t end_bit) {
   const int passes = (end_bit - begin_bit + kRadixBits - 1) / kRadixBits;
   return passes > 0 ? (end_bit - begin_bit + passes - 1) / passes : 0;
@@ -2343,7 +2380,7 @@ gs_status gs_depth_sort_msd(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, 
   k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, totals, nb);
   k_radix_scatter<true><<<nb, kBlock, 0, s>>>(keys, nullptr, keys_alt, vals_alt, n, shift, kRadixBits, counts,
                                                totals, nb);
-  k_msd_bucket_sort<<<kRadix - 1, kMsdThreads, 0, s>>>(keys_alt, vals_alt, totals, shift, overflow_word);
+  k_msd_bucket_sort<false><<<kRadix - 1, kMsdThreads, 0, s>>>(keys_alt, vals_alt, totals, shift, overflow_word);
   return check_launch("gs_depth_sort_msd");
 }
 

@@ -508,17 +508,21 @@ def test_emit_capacity_guess(pkg, cuda):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("guess", ["last", 16])
-def test_frame_entry_points_match(pkg, cuda, guess):
+@pytest.mark.parametrize("guess,scene", [("last", "40k"), (16, "40k"), ("last", "5k"), ("last", "5k_wide")])
+def test_frame_entry_points_match(pkg, cuda, guess, scene):
     """The default tile renders through the frame entry points
     (gs_render_forward / gs_render_backward, one library call per direction);
     the stage-by-stage path (GS_FRAME_CALLS=0, every other tile size) launches
     the same kernels: outputs, gradients and the frame's index work are
     bit-identical -- with a capacity guess that holds, and one far too small
-    (GS_NEED_CAPACITY, then the call resumed with a larger tile workspace)."""
+    (GS_NEED_CAPACITY, then the call resumed with a larger tile workspace).
+    Small frames (5k: n and T within one workgroup's sort; 5k_wide: n within
+    it, T not) sort in one launch there (gs_internal_small_sort), with the
+    radix passes' result."""
     RZ = pkg.rasterizer
     syn = pkg.synthetic
-    sc = syn.make_scene(40000, 480, 270, seed=8, sigma_range=(0.002, 0.02))
+    n, sig = {"40k": (40000, (0.002, 0.02)), "5k": (5000, (0.002, 0.01)), "5k_wide": (5000, (0.02, 0.06))}[scene]
+    sc = syn.make_scene(n, 480, 270, seed=8, sigma_range=sig)
     res = []
     saved = RZ._FRAME_CALLS
     try:
@@ -529,6 +533,9 @@ def test_frame_entry_points_match(pkg, cuda, guess):
                 RZ._T_SEEN[cuda] = guess
             out = pkg.GaussianRenderer().render(Cam(480, 270, sc.fovx, sc.fovy), m,
                                                 pkg.RenderSettings(270, 480, torch.tensor([0.1, 0.2, 0.3])))
+            if fast and scene != "40k":
+                T = RZ._T_SEEN[cuda]
+                assert (T <= 16384) == (scene == "5k"), T
             (out["image"].sum() + out["alpha"].mean() + out["depth"].mean() + out["viewspace_points"].sum()).backward()
             res.append([out[k].clone() for k in ("image", "alpha", "depth", "viewspace_points", "radii", "conics",
                                                  "visibility_filter")] +
