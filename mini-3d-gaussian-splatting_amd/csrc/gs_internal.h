@@ -4,7 +4,10 @@
 
 // entries per radix sort block (gsplat_mi355x.hip kSortChunk): the row length
 // of the sort's digit-count table is div_up(n, kSortBlockEntries)
-constexpr int32_t kSortBlockEntries = 2048;
+#ifndef GS_SORT_IPT
+#define GS_SORT_IPT 8
+#endif
+constexpr int32_t kSortBlockEntries = 256 * GS_SORT_IPT;
 
 // set gs_last_error() (fmt has one %s, filled with `what`) and return s
 __attribute__((visibility("hidden"))) gs_status gs_internal_fail(gs_status s, const char *fmt, const char *what);
