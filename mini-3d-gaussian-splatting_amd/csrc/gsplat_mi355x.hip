@@ -155,6 +155,42 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *s_tmp, ui
   return base + incl - v;
 }
 
+// Three exclusive scans over the block at once (one round of shuffles and
+// barriers for all three: the single-block scans are latency-bound).
+__device__ __forceinline__ uint3 block_exscan3(uint3 v, uint32_t (*s_tmp)[kBlock / kWave], uint3 *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint3 incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t tx = __shfl_up(incl.x, d, 64), ty = __shfl_up(incl.y, d, 64), tz = __shfl_up(incl.z, d, 64);
+    if (lane >= d) {
+      incl.x += tx;
+      incl.y += ty;
+      incl.z += tz;
+    }
+  }
+  if (lane == 63) {
+    s_tmp[0][wave] = incl.x;
+    s_tmp[1][wave] = incl.y;
+    s_tmp[2][wave] = incl.z;
+  }
+  __syncthreads();
+  uint3 base = make_uint3(0u, 0u, 0u), tot = make_uint3(0u, 0u, 0u);
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) {
+    const uint32_t x = s_tmp[0][w], y = s_tmp[1][w], z = s_tmp[2][w];
+    base.x += (w < wave) ? x : 0u;
+    base.y += (w < wave) ? y : 0u;
+    base.z += (w < wave) ? z : 0u;
+    tot.x += x;
+    tot.y += y;
+    tot.z += z;
+  }
+  __syncthreads();
+  *total = tot;
+  return make_uint3(base.x + incl.x - v.x, base.y + incl.y - v.y, base.z + incl.z - v.z);
+}
+
 // Lanes of the wave holding the same `nbits`-bit digit (match-any via ballots).
 __device__ __forceinline__ unsigned long long match_digit(uint32_t d, int nbits, unsigned long long m) {
   for (int b = 0; b < nbits; ++b) {
@@ -768,7 +804,7 @@ struct TileHist {
 };
 
 __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t *partials, int nb, TileHist th) {
-  __shared__ uint32_t s_tmp[4];
+  __shared__ uint32_t s_tmp3[3][kBlock / kWave];
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < th.zero_words; i += gridDim.x * kBlock) th.counts[i] = 0u;
   const long long base = (long long)blockIdx.x * kBinChunk;
   constexpr int kR = kBinChunk / kBlock;
@@ -803,12 +839,25 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
       nvis += vis_o[i] ? 1u : 0u;
     }
   }
-  uint32_t tot, totv;
-  block_exscan(sum, s_tmp, &tot);
-  block_exscan(nvis, s_tmp, &totv);
+  // Gradient slots are numbered in Gaussian-index order (a Gaussian's
+  // touches consecutive), so that gs_project_backward's threads g, g+1 read
+  // adjacent slot ranges: here each Gaussian's exclusive prefix of touches
+  // inside this block's index chunk (k_bin_emit adds the chunk's offset).
+  uint32_t cnt[kR];
+#pragma unroll
+  for (int i = 0; i < kR; ++i) {
+    const long long g = base + i * kBlock + threadIdx.x;
+    cnt[i] = g < a.n ? rect_touches((int)(rc_own[i].x & 0xFFFFu), (int)(rc_own[i].x >> 16),
+                                    (int)(rc_own[i].y & 0xFFFFu), (int)(rc_own[i].y >> 16))
+                     : 0u;
+  }
+  // the block's touches (depth order) and visible count, and round 0's slot
+  // prefix, in one scan
+  uint3 t3;
+  const uint3 e3 = block_exscan3(make_uint3(sum, nvis, cnt[0]), s_tmp3, &t3);
   if (threadIdx.x == 0) {
-    partials[blockIdx.x] = tot;
-    partials[nb + blockIdx.x] = totv;
+    partials[blockIdx.x] = t3.x;
+    partials[nb + blockIdx.x] = t3.y;
   }
   // the depth-ordered rectangles, for k_bin_emit to read coalesced
   uint2 *srect = sorted_rects(partials, nb);
@@ -817,21 +866,18 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
     const long long k = base + i * kBlock + threadIdx.x;
     if (k < a.n) srect[k] = rc_d[i];
   }
-  // Gradient slots are numbered in Gaussian-index order (a Gaussian's
-  // touches consecutive), so that gs_project_backward's threads g, g+1 read
-  // adjacent slot ranges: here each Gaussian's exclusive prefix of touches
-  // inside this block's index chunk (k_bin_emit adds the chunk's offset).
+  // rounds 1..3's prefixes in one more scan (integer sums: any grouping)
+  static_assert(kR == 4, "the slot prefix scans assume four rounds per binning block");
+  uint3 u3;
+  const uint3 f3 = block_exscan3(make_uint3(cnt[1], cnt[2], cnt[3]), s_tmp3, &u3);
+  const uint32_t ex[kR] = {e3.z, f3.x, f3.y, f3.z};
+  const uint32_t tt[kR] = {t3.z, u3.x, u3.y, u3.z};
   uint32_t carry = 0;
 #pragma unroll
   for (int i = 0; i < kR; ++i) {
     const long long g = base + i * kBlock + threadIdx.x;
-    const uint32_t cnt = g < a.n ? rect_touches((int)(rc_own[i].x & 0xFFFFu), (int)(rc_own[i].x >> 16),
-                                                (int)(rc_own[i].y & 0xFFFFu), (int)(rc_own[i].y >> 16))
-                                 : 0u;
-    uint32_t t;
-    const uint32_t ex = block_exscan(cnt, s_tmp, &t);
-    if (g < a.n) a.pair_offset[g] = carry + ex;
-    carry += t;
+    if (g < a.n) a.pair_offset[g] = carry + ex[i];
+    carry += tt[i];
   }
   if (threadIdx.x == 0) partials[2 * nb + blockIdx.x] = carry;
   // the projection blocks of this chunk (kBinChunk / kBlock of them): their
@@ -857,10 +903,10 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
 // [2] / [3] = min / max visible depth bits (the projection's per-block values)
 __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials, int nb, uint32_t *counters,
                                                                uint32_t *host_counters, uint32_t host_seq) {
-  __shared__ uint32_t s_tmp[4];
+  __shared__ uint32_t s_tmp3[3][kBlock / kWave];
   __shared__ uint32_t s_mm[2][kBlock / kWave];
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-  uint32_t carry = 0, vis = 0, slots = 0, tot;
+  uint32_t carry = 0, vis = 0, slots = 0;
   // a chunk's three partials loaded unconditionally (clamped index) and the
   // next chunk's in flight during this one's scans: no load waits under a
   // branch (the compiler waited for each conditional load at its join)
@@ -881,15 +927,17 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
     mn = min(mn, vn[3]);
     mx = max(mx, vn[4]);
     ld(i + kBlock, vn);
-    const uint32_t e0 = block_exscan(v0, s_tmp, &tot);
-    if (i < nb) partials[i] = carry + e0;
-    carry += tot;
-    block_exscan(v1, s_tmp, &tot);
-    vis += tot;
-    // index-order slot chunks (k_bin_partials): exclusive offsets in place
-    const uint32_t e2 = block_exscan(v2, s_tmp, &tot);
-    if (i < nb) partials[2 * nb + i] = slots + e2;
-    slots += tot;
+    // touches (depth order), visible, index-order slot chunks (k_bin_partials):
+    // exclusive offsets of the first and third in place
+    uint3 t3;
+    const uint3 e = block_exscan3(make_uint3(v0, v1, v2), s_tmp3, &t3);
+    if (i < nb) {
+      partials[i] = carry + e.x;
+      partials[2 * nb + i] = slots + e.z;
+    }
+    carry += t3.x;
+    vis += t3.y;
+    slots += t3.z;
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
@@ -966,6 +1014,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   __shared__ uint32_t s_g[kBlock];
   __shared__ uint2 s_rect[kBlock];
   __shared__ uint32_t s_tmp[4];
+  __shared__ uint32_t s_tmp3[3][kBlock / kWave];
   __shared__ uint8_t s_owner[kOwnerCap];
   __shared__ uint32_t s_hist[kHistSpan * kRadix];
   // T entries do not fit: do nothing (the caller re-emits into T-sized
@@ -981,7 +1030,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   const uint32_t hb0 = out_base / kSortChunk;
   if (hist) {
     for (int i = threadIdx.x; i < kHistSpan * kRadix; i += kBlock) s_hist[i] = 0u;
-    // (ordered before the first use by the barrier inside the first round's scan)
+    // (ordered before the first use by the barriers inside the prefix scans)
   }
   constexpr int kR = kBinChunk / kBlock;
   // all rounds' ids and rects unconditionally (clamped): one round trip for
@@ -998,18 +1047,32 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
     rcr[r] = srect[kc];  // (k_bin_partials' depth-ordered copy: no gather by id)
     offr[r] = a.pair_offset[kc];  // (index order, for the slot pass below)
   }
+  // every round's touch counts and their prefixes up front (three rounds in
+  // one scan: the scans are latency-bound)
+  static_assert(kR == 4, "the emission's prefix scans assume four rounds per binning block");
+  uint32_t cntr[kR];
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     const long long k = base + r * kBlock + threadIdx.x;
-    uint32_t g = 0xFFFFFFFFu, cnt = 0;
-    uint2 rc = make_uint2(1u, 1u);
     if (k < a.n) {
-      g = gr[r];
-      rc = rcr[r];
-      cnt = rect_touches((int)(rc.x & 0xFFFFu), (int)(rc.x >> 16), (int)(rc.y & 0xFFFFu), (int)(rc.y >> 16));
+      cntr[r] = rect_touches((int)(rcr[r].x & 0xFFFFu), (int)(rcr[r].x >> 16), (int)(rcr[r].y & 0xFFFFu),
+                             (int)(rcr[r].y >> 16));
+    } else {
+      cntr[r] = 0u;
+      gr[r] = 0xFFFFFFFFu;
+      rcr[r] = make_uint2(1u, 1u);
     }
-    uint32_t tot;
-    const uint32_t ex = block_exscan(cnt, s_tmp, &tot);  // barrier inside: previous round done
+  }
+  uint3 ta;
+  uint32_t tb;
+  const uint3 ea = block_exscan3(make_uint3(cntr[0], cntr[1], cntr[2]), s_tmp3, &ta);
+  const uint32_t eb = block_exscan(cntr[3], s_tmp, &tb);
+  const uint32_t exr[kR] = {ea.x, ea.y, ea.z, eb}, totr[kR] = {ta.x, ta.y, ta.z, tb};
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const uint32_t g = gr[r], cnt = cntr[r], ex = exr[r], tot = totr[r];
+    const uint2 rc = rcr[r];
+    if (r) __syncthreads();  // the previous round's owner-map and offset reads are done
     s_off[threadIdx.x] = ex;
     s_g[threadIdx.x] = g;
     s_rect[threadIdx.x] = rc;
