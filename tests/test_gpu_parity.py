@@ -508,7 +508,8 @@ def test_emit_capacity_guess(pkg, cuda):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("guess,scene", [("last", "40k"), (16, "40k"), ("last", "5k"), ("last", "5k_wide")])
+@pytest.mark.parametrize("guess,scene", [("last", "40k"), (16, "40k"), ("last", "5k"), (16, "5k"), ("last", "5k_wide"),
+                                         ("last", "16384"), ("last", "16385")])
 def test_frame_entry_points_match(pkg, cuda, guess, scene):
     """The default tile renders through the frame entry points
     (gs_render_forward / gs_render_backward, one library call per direction);
@@ -521,7 +522,9 @@ def test_frame_entry_points_match(pkg, cuda, guess, scene):
     radix passes' result."""
     RZ = pkg.rasterizer
     syn = pkg.synthetic
-    n, sig = {"40k": (40000, (0.002, 0.02)), "5k": (5000, (0.002, 0.01)), "5k_wide": (5000, (0.02, 0.06))}[scene]
+    n, sig = {"40k": (40000, (0.002, 0.02)), "5k": (5000, (0.002, 0.01)), "5k_wide": (5000, (0.02, 0.06)),
+              # the one-workgroup depth sort's edge (gs_internal_small_sort: n <= 16384)
+              "16384": (16384, (0.002, 0.01)), "16385": (16385, (0.002, 0.01))}[scene]
     sc = syn.make_scene(n, 480, 270, seed=8, sigma_range=sig)
     res = []
     saved = RZ._FRAME_CALLS
@@ -533,7 +536,7 @@ def test_frame_entry_points_match(pkg, cuda, guess, scene):
                 RZ._T_SEEN[cuda] = guess
             out = pkg.GaussianRenderer().render(Cam(480, 270, sc.fovx, sc.fovy), m,
                                                 pkg.RenderSettings(270, 480, torch.tensor([0.1, 0.2, 0.3])))
-            if fast and scene != "40k":
+            if fast and scene in ("5k", "5k_wide"):
                 T = RZ._T_SEEN[cuda]
                 assert (T <= 16384) == (scene == "5k"), T
             (out["image"].sum() + out["alpha"].mean() + out["depth"].mean() + out["viewspace_points"].sum()).backward()
