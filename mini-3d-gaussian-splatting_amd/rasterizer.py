@@ -61,9 +61,8 @@ class CameraParams:
     @property
     def groups(self) -> int:
         """Gradient partials a one-batch blend backward writes per list entry
-        (gs_partial_groups): 1 at the default tile (its four cells combined
-        on chip), else one per cell.  Tiles of many cells may replay them in
-        batches (frame_groups)."""
+        (gs_partial_groups): one per 8x8 cell, 4 at the default tile.  Tiles
+        of many cells may replay them in batches (frame_groups)."""
         return _partial_groups(self.tile_size)
 
     def frame_groups(self, entries: int) -> int:
@@ -72,6 +71,19 @@ class CameraParams:
         return self.groups if self.groups < self.cells else cell_batch(self.cells, entries)
 
     def to_struct(self) -> N.GsCamera:
+        """The ABI camera (cached per distinct value set: building it costs
+        ~5-10 us of host time per frame; callers copy it into their
+        argument structs and never modify it)."""
+        key = (self.image_width, self.image_height, self.fx, self.fy, self.cx, self.cy, self.view, self.bg,
+               self.radius_min, self.radius_max, self.tile_size)
+        c = _CAM_STRUCTS.get(key)
+        if c is None:
+            if len(_CAM_STRUCTS) >= 4096:
+                _CAM_STRUCTS.clear()
+            c = _CAM_STRUCTS[key] = self._build_struct()
+        return c
+
+    def _build_struct(self) -> N.GsCamera:
         c = N.GsCamera()
         c.image_width, c.image_height = int(self.image_width), int(self.image_height)
         c.fx, c.fy, c.cx, c.cy = self.fx, self.fy, self.cx, self.cy
@@ -93,6 +105,7 @@ class CameraParams:
 
 
 _GROUPS: dict = {}
+_CAM_STRUCTS: dict = {}  # CameraParams values -> GsCamera (CameraParams.to_struct)
 
 
 def _partial_groups(tile_size: int) -> int:
@@ -151,8 +164,29 @@ def _rows(t: torch.Tensor, cols: int) -> Tuple[torch.Tensor, int]:
     return t, t.stride(0)
 
 
+_G_STRUCTS: dict = {}  # (pointers, strides, flags) -> GsGaussians (_gaussians_struct)
+
+
 def _gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
                       sh_rest=None, sh_degree=0) -> N.GsGaussians:
+    """The ABI view of the Gaussians' tensors, cached by the addresses,
+    strides and flags it holds (the same model renders with the same struct;
+    callers copy it and never modify it)."""
+    key = (n, xyz.data_ptr(), xyz.stride(0), None if cov3d is None else cov3d.data_ptr(),
+           None if scaling is None else scaling.data_ptr(), None if rotation is None else rotation.data_ptr(),
+           logits.data_ptr(), logits.stride(0), opacity.data_ptr(), opacity.stride(0), bool(opacity_is_logit),
+           int(sh_degree), None if sh_rest is None or sh_degree <= 0 else (sh_rest.data_ptr(), sh_rest.stride(0)))
+    g = _G_STRUCTS.get(key)
+    if g is None:
+        if len(_G_STRUCTS) >= 4096:
+            _G_STRUCTS.clear()
+        g = _G_STRUCTS[key] = _build_gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity,
+                                                      opacity_is_logit, sh_rest, sh_degree)
+    return g
+
+
+def _build_gaussians_struct(n, xyz, cov3d, scaling, rotation, logits, opacity, opacity_is_logit=False,
+                            sh_rest=None, sh_degree=0) -> N.GsGaussians:
     g = N.GsGaussians()
     g.n = n
     g.xyz, g.xyz_stride = N.ptr(xyz), xyz.stride(0)

@@ -79,11 +79,15 @@ def effective_tile(tile_size: int, width: int, height: int) -> int:
 def _host_f32(t, count: int) -> list:
     """The values of `t` (a tensor or sequence of `count` numbers) rounded to
     fp32, as Python floats, row-major (a CPU fp32 tensor is read as is)."""
-    t = torch.as_tensor(t)
-    if t.device.type != "cpu" or t.dtype != torch.float32:
-        t = t.detach().to("cpu", torch.float32)
+    if not isinstance(t, torch.Tensor) or t.device.type != "cpu" or t.dtype != torch.float32:
+        t = torch.as_tensor(t).detach().to("cpu", torch.float32)
     if t.numel() != count:
         raise ValueError(f"expected {count} values, got a tensor of shape {tuple(t.shape)}")
+    d = t.dim()
+    if d == 1:
+        return t.tolist()
+    if d == 2:  # (a 4x4 view matrix: tolist and flatten, 1 us instead of reshape + tolist's 3)
+        return [v for row in t.tolist() for v in row]
     return t.reshape(count).tolist()
 
 
