@@ -198,3 +198,34 @@ def test_render_input_validation(pkg, monkeypatch):
     # fp64 passes validation (cast), then reaches the launch path (camera None here)
     with pytest.raises(AttributeError):
         call(logits=torch.zeros(n, 3, dtype=torch.float64))
+
+
+def test_host_scalars_and_struct_caches(pkg):
+    """camera_params reads the view and background as fp32 values from any
+    tensor / sequence form; the ABI structs cached by value
+    (CameraParams.to_struct, rasterizer._gaussians_struct) follow every
+    change of what they hold."""
+    import torch
+    R, RZ = pkg.renderer, pkg.rasterizer
+    wv = torch.arange(16, dtype=torch.float64).reshape(4, 4) / 7
+    want = [float(v) for v in wv.float().reshape(-1)]
+    assert R._host_f32(wv, 16) == want
+    assert R._host_f32(wv.float(), 16) == want
+    assert R._host_f32(wv.float().reshape(-1), 16) == want
+    assert R._host_f32([0.1, 0.2, 0.3], 3) == [float(v) for v in torch.tensor([0.1, 0.2, 0.3])]
+    with pytest.raises(ValueError):
+        R._host_f32(torch.zeros(3, 3), 16)
+    cp = RZ.CameraParams(64, 48, 50.0, 50.0, 32.0, 24.0, tuple(range(12)), (0.0, 0.5, 1.0))
+    a = cp.to_struct()
+    assert a is cp.to_struct() and (a.image_width, a.image_height, a.bg[1]) == (64, 48, 0.5)
+    cp2 = RZ.CameraParams(64, 48, 50.0, 50.0, 32.0, 24.0, tuple(range(12)), (0.0, 0.25, 1.0))
+    assert cp2.to_struct().bg[1] == 0.25 and a.bg[1] == 0.5
+    xyz, sc, rot = torch.zeros(5, 3), torch.zeros(5, 3), torch.zeros(5, 4)
+    col, op = torch.zeros(5, 1, 3), torch.zeros(5, 1)
+    g = RZ._gaussians_struct(5, xyz, None, sc, rot, col, op, True)
+    assert g is RZ._gaussians_struct(5, xyz, None, sc, rot, col, op, True)
+    assert (g.xyz, g.color_logits, g.color_stride, g.opacity_is_logit) == (xyz.data_ptr(), col.data_ptr(), 3, 1)
+    g2 = RZ._gaussians_struct(5, xyz, None, sc, rot, col, op, False)
+    assert g2.opacity_is_logit == 0 and g.opacity_is_logit == 1
+    xyz2 = torch.zeros(5, 3)
+    assert RZ._gaussians_struct(5, xyz2, None, sc, rot, col, op, True).xyz == xyz2.data_ptr()
