@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 21
+#define GS_ABI_VERSION 20
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 4096      /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
                                  of at least max(W, H) renders the same as any larger one (one tile
@@ -140,9 +140,6 @@ typedef struct gs_project_args {
   int32_t key_bits;     /* 1..32 */
   uint32_t *key_minmax; /* [2 * ceil(n / 256)] per-block min / max of the visible bits(Z), for
                            gs_bin_count's counters[2..3] */
-  float *cull;          /* optional [n,4] (NULL: not written): per visible Gaussian the blend
-                           forward's cell-culling bounds (gs_blend_fwd_args.cull) -- the same
-                           values the blend would compute per (entry, cell) batch, once */
 } gs_project_args;
 gs_status gs_project_forward(const gs_project_args *a, gs_stream_t stream);
 
@@ -267,8 +264,6 @@ typedef struct gs_blend_fwd_args {
   uint32_t *pix_neval;          /* [H*W] or NULL: each pixel's evaluated entries (the work counter
                                    E of SURVEY 8(d), and the oracle's decision-forced replay);
                                    measurement only */
-  const float *cull;            /* optional: gs_project_args.cull of the same projection (NULL: each
-                                   batch computes the bounds itself; the same decisions either way) */
 } gs_blend_fwd_args;
 gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream);
 

@@ -27,7 +27,7 @@ GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
 GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 21
+GS_ABI_VERSION = 20
 GS_NEED_CAPACITY, GS_RETRY_FULL_KEYS = 4, 5  # gs_render_forward: what to do next (not errors)
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
@@ -56,7 +56,7 @@ class GsProjectArgs(C.Structure):
     _fields_ = [
         ("cam", GsCamera), ("g", GsGaussians), ("means2d", _vp), ("conics", _vp), ("radii", _vp),
         ("vis", _vp), ("records", _vp), ("rects", _vp), ("depth_keys", _vp),
-        ("key_base", C.c_uint32), ("key_bits", C.c_int32), ("key_minmax", _vp), ("cull", _vp),
+        ("key_base", C.c_uint32), ("key_bits", C.c_int32), ("key_minmax", _vp),
     ]
 
 
@@ -82,7 +82,7 @@ class GsBlendFwdArgs(C.Structure):
         ("cam", GsCamera), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32), ("ranges", _vp),
         ("sorted_gauss", _vp), ("records", _vp), ("image", _vp), ("alpha", _vp), ("depth", _vp),
         ("pix_flags", _vp), ("cell_neval", _vp), ("live_bits", _vp), ("live_words", C.c_int64),
-        ("pair_counts", _vp), ("num_pairs", C.c_int32), ("pix_neval", _vp), ("cull", _vp),
+        ("pair_counts", _vp), ("num_pairs", C.c_int32), ("pix_neval", _vp),
     ]
 
 

@@ -28,7 +28,7 @@ size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // frame_ws: per-Gaussian and per-pixel buffers (offsets in bytes)
 struct FrameLayout {
   size_t records, rects, keys, vals, key_minmax, counters, sort_ws, bin_ws, pair_offset, ranges, pix_flags,
-      cell_neval, grad_sums, cull, total;
+      cell_neval, grad_sums, total;
 };
 
 FrameLayout frame_layout(int32_t n, int32_t W, int32_t H, int32_t tiles, int32_t cells) {
@@ -53,7 +53,6 @@ FrameLayout frame_layout(int32_t n, int32_t W, int32_t H, int32_t tiles, int32_t
   L.pix_flags = take(hw);
   L.cell_neval = take((size_t)tiles * (size_t)(cells > 0 ? cells : 0) * 4);
   L.grad_sums = take(un * GS_PAIR_GRAD_FLOATS * 4);
-  L.cull = take(un * 16);  // the blend's culling bounds per Gaussian (gs_project_args.cull)
   L.total = o;
   return L;
 }
@@ -173,7 +172,6 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
     pa.key_base = a->key_base;
     pa.key_bits = a->key_bits;
     pa.key_minmax = key_minmax;
-    pa.cull = reinterpret_cast<float *>(fw + F.cull);
     if ((st = gs_project_forward(&pa, stream))) return st;
     if (n == 0) return GS_OK;
     int32_t alt = 0;
@@ -286,7 +284,6 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   fa.pix_flags = reinterpret_cast<uint8_t *>(fw + F.pix_flags);
   fa.cell_neval = reinterpret_cast<uint32_t *>(fw + F.cell_neval);
   fa.pix_neval = a->pix_neval;
-  fa.cull = reinterpret_cast<const float *>(fw + F.cull);
   fa.live_bits = a->fb.live_cells > 0 ? reinterpret_cast<uint64_t *>(tw + T0.live) : nullptr;
   fa.live_words = (int64_t)T0.live_words;
   fa.pair_counts = a->pair_counts;

@@ -126,23 +126,6 @@ __device__ __forceinline__ float conic_s(float dx, float dy, float q00, float qo
   return ((dx * dx) * q00 + (qo * dx) * dy) + (dy * dy) * q11;
 }
 
-// The per-Gaussian part of the blend forward's cell culling (cell_hit, below)
-// -- the conditioning check, the box half-extents and the edge minimisers'
-// slopes -- depends on the conic alone: cull_bounds computes it (in the
-// projection, once per Gaussian, or in the blend per batch), cell_hit_b
-// applies it to a cell.  hx < 0: never culled.
-__device__ __forceinline__ float4 cull_bounds(float q00, float qo, float q11) {
-  const float q01 = 0.5f * qo;
-  const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
-  if (!(tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det)) return make_float4(-1.f, 0.f, 0.f, 0.f);
-  const float L = 23.1f * 1.01f;
-  // v_rcp / v_sqrt (~1 ulp): far inside the 1% margin
-  const float id = __builtin_amdgcn_rcpf(det);
-  const float hx = __builtin_amdgcn_sqrtf(L * q11 * id), hy = __builtin_amdgcn_sqrtf(L * q00 * id);
-  const float kx = -0.5f * qo * __builtin_amdgcn_rcpf(q11), ky = -0.5f * qo * __builtin_amdgcn_rcpf(q00);
-  return make_float4(hx, hy, kx, ky);
-}
-
 __device__ __forceinline__ unsigned long long lanemask_lt() {
   const int lane = threadIdx.x & (kWave - 1);
   return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -459,8 +442,6 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
       rec[0] = make_float4(mx, my, q0, q3);
       rec[1] = make_float4(q1 + q2, op, cr, cg);
       rec[2] = make_float4(cb, Z, 0.f, __uint_as_float(rinfo));
-      // (from the record's own fp32 conic words: the values the blend would compute)
-      if (a.cull) reinterpret_cast<float4 *>(a.cull)[g] = cull_bounds(q0, q1 + q2, q3);
     }
     reinterpret_cast<uint2 *>(a.rects)[g] = make_uint2(rx, ry);
     zbits = __float_as_uint(Z);
@@ -1222,11 +1203,14 @@ __device__ __forceinline__ float2 lds_pair(const float2 *p) {
 // s: |s_fp32 - s| <= ~4u (q00 dx^2 + |qo dx dy| + q11 dy^2) <= 4u (tr + |qo|)
 // tr / det * s, so conics with (tr + |qo|) tr > 1e4 det -- and
 // non-positive-definite or NaN ones -- are never culled.
-__device__ __forceinline__ bool cell_hit_b(float mx, float my, float q00, float qo, float q11, float4 b, float x0,
-                                           float y0) {
-  if (!(b.x >= 0.f)) return true;
+__device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo, float q11, float x0, float y0) {
+  const float q01 = 0.5f * qo;
+  const float det = q00 * q11 - q01 * q01, tr = q00 + q11;
+  if (!(tr > 0.f && det > 0.f && (tr + fabsf(qo)) * tr <= 1e4f * det)) return true;
   const float L = 23.1f * 1.01f;
-  const float hx = b.x, hy = b.y;
+  // v_rcp / v_sqrt (~1 ulp): far inside the 1% margin
+  const float id = __builtin_amdgcn_rcpf(det);
+  const float hx = __builtin_amdgcn_sqrtf(L * q11 * id), hy = __builtin_amdgcn_sqrtf(L * q00 * id);
   const bool box = mx + hx >= x0 && mx - hx <= x0 + 7.f && my + hy >= y0 && my - hy <= y0 + 7.f;
   if (!box) return false;
   // The ellipse's bounding box meets the cell: the minimum of s over the
@@ -1238,17 +1222,13 @@ __device__ __forceinline__ bool cell_hit_b(float mx, float my, float q00, float 
   // relative error as above, inside the 1% margin.
   const float ax0 = x0 - mx, ax1 = x0 + 7.f - mx, ay0 = y0 - my, ay1 = y0 + 7.f - my;
   if (ax0 <= 0.f && ax1 >= 0.f && ay0 <= 0.f && ay1 >= 0.f) return true;
-  const float kx = b.z, ky = b.w;
+  const float kx = -0.5f * qo * __builtin_amdgcn_rcpf(q11), ky = -0.5f * qo * __builtin_amdgcn_rcpf(q00);
   auto sv = [&](float dx, float dy) { return (dx * dx) * q00 + (qo * dx) * dy + (dy * dy) * q11; };
   const float e0 = sv(ax0, __builtin_amdgcn_fmed3f(kx * ax0, ay0, ay1));
   const float e1 = sv(ax1, __builtin_amdgcn_fmed3f(kx * ax1, ay0, ay1));
   const float e2 = sv(__builtin_amdgcn_fmed3f(ky * ay0, ax0, ax1), ay0);
   const float e3 = sv(__builtin_amdgcn_fmed3f(ky * ay1, ax0, ax1), ay1);
   return fminf(fminf(e0, e1), fminf(e2, e3)) <= L;
-}
-
-__device__ __forceinline__ bool cell_hit(float mx, float my, float q00, float qo, float q11, float x0, float y0) {
-  return cell_hit_b(mx, my, q00, qo, q11, cull_bounds(q00, qo, q11), x0, y0);
 }
 
 // Workgroup b -> (tile, cell) and the tile's list range: b, b+8, b+16, ...
@@ -1332,16 +1312,12 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
   // (no bitmap: the caller's budget; the backward then replays every entry)
   uint64_t *live = a.live_bits ? a.live_bits + (size_t)quad * a.live_words + start / 64u + (uint32_t)tile : nullptr;
   const uint64_t live_left = a.live_bits ? (uint64_t)a.live_words - (start / 64u + (uint32_t)tile) : 0u;
-  // the projection's culling bounds, when given, come with each record
-  // (cull_bounds: the same values as computed here per batch)
-  const float4 *cullb = reinterpret_cast<const float4 *>(a.cull);
-  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0, nc = n0;
+  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
   if (start + (uint32_t)lane < end) {
     const uint32_t gid = a.sorted_gauss[start + lane];
     n0 = recs[3 * (size_t)gid];
     n1 = recs[3 * (size_t)gid + 1];
     n2 = recs[3 * (size_t)gid + 2];
-    if (cullb) nc = cullb[gid];
   }
   for (uint32_t b = start; b < end; b += kWave) {
     if (!wave_any(A < kAlphaStop)) break;  // every pixel of the cell done
@@ -1350,9 +1326,7 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
     d[0] = n0;
     d[1] = n1;
     d[2] = n2;
-    const bool hit = b + (uint32_t)lane < end &&
-                     (cullb ? cell_hit_b(n0.x, n0.y, n0.z, n1.x, n0.w, nc, (float)x0, (float)y0)
-                            : cell_hit(n0.x, n0.y, n0.z, n1.x, n0.w, (float)x0, (float)y0));
+    const bool hit = b + (uint32_t)lane < end && cell_hit(n0.x, n0.y, n0.z, n1.x, n0.w, (float)x0, (float)y0);
     const unsigned long long mw = __builtin_amdgcn_ballot_w64(hit);
     unsigned long long m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mw >> 32)) << 32) |
                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mw);
@@ -1364,7 +1338,6 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
       n0 = recs[3 * (size_t)gid];
       n1 = recs[3 * (size_t)gid + 1];
       n2 = recs[3 * (size_t)gid + 2];
-      if (cullb) nc = cullb[gid];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
     unsigned long long livem = 0;  // entries some lane of this cell evaluated

@@ -641,13 +641,12 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
     vals = torch.empty((2, n), dtype=i32, device=dev)
     counters = torch.empty((N.GS_NUM_COUNTERS,), dtype=i32, device=dev)
     key_minmax = torch.empty((2 * max(1, (n + 255) // 256),), dtype=i32, device=dev)
-    cull = torch.empty((n, 4), dtype=f32, device=dev)  # the blend's per-Gaussian culling bounds
     window = _window_for(dev) if depth_window_ok else None
     key_base, key_bits = window if window is not None else (0, 32)
 
     StageTimer.mark("project_fwd")
     pa = N.GsProjectArgs(cs, gst, N.ptr(means2d), N.ptr(conics), N.ptr(radii), N.ptr(vis), N.ptr(records),
-                         N.ptr(rects), N.ptr(keys[0]), key_base, key_bits, N.ptr(key_minmax), N.ptr(cull))
+                         N.ptr(rects), N.ptr(keys[0]), key_base, key_bits, N.ptr(key_minmax))
     N.check(lib.gs_project_forward(C.byref(pa), s), "gs_project_forward")
 
     fr = _Frame()
@@ -773,7 +772,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
 
     fa = N.GsBlendFwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(ranges), L.p_tv[alt.value], N.ptr(records),
                           N.ptr(image), N.ptr(alpha), N.ptr(depth), N.ptr(pix_flags), N.ptr(cell_neval),
-                          L.p_live, L.live_words, N.ptr(pair_counts), T, N.ptr(pix_neval), N.ptr(cull))
+                          L.p_live, L.live_words, N.ptr(pair_counts), T, N.ptr(pix_neval))
     StageTimer.mark("blend_fwd")
     N.check(lib.gs_blend_forward(C.byref(fa), s), "gs_blend_forward")
     StageTimer.mark("~end_fwd")
