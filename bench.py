@@ -57,12 +57,15 @@ CONFIGS = {"C1": (5_000, 256, 256), "C2": (100_000, 800, 800), "C3": (1_000_000,
 # steps only ~15 ms.  (C1 is host-bound; its step time varies 0.21-0.39 ms
 # between runs on the same box whatever the spin-up, profiles/r05/host/.)
 SPINUP_STEPS = {"C1": 1000, "C2": 300, "C3": 50, "4K": 20}
+TIMED_STEPS = {"C1": 500, "C2": 200, "C3": 30, "4K": 30}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 30 at C3; more for the small presets, whose ~0.3 ms steps "
+                         "would otherwise time a ~10 ms window that one host preemption skews)")
     ap.add_argument("--warmup", type=int, default=10)  # (clocks and allocator settle: a 3-step warmup once timed 20 % slow)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="C3",
                     help="workload preset (BASELINE.json configs; C3 = the metric's, the default)")
@@ -93,6 +96,8 @@ def parse():
     a.height = h0 if a.height is None else a.height
     if a.spinup_steps is None:
         a.spinup_steps = SPINUP_STEPS.get(a.config, 50)
+    if a.steps is None:
+        a.steps = TIMED_STEPS.get(a.config, 30)
     return a
 
 
