@@ -841,6 +841,26 @@ def test_sparse_frame_vs_oracle(pkg, cuda):
     assert not errs, errs
 
 
+@pytest.mark.parametrize("bg", [(0.95, 0.6, 0.0), (1.0, 1.0, 1.0)])
+def test_clamped_pixels_vs_oracle(pkg, cuda, bg):
+    """Composites that leave [0, 1]: the blend backward reads its per-pixel
+    state from the forward's outputs and a clamp-flag byte (round 5), so a
+    blocked channel's gradient must come from the flag, not from the
+    clamped image.  A bright background (counted twice, renderer.py:273,
+    :359) saturates many pixels' red channel; white saturates all three."""
+    W, H = 160, 120
+    sc = pkg.synthetic.make_scene(6000, W, H, seed=77, sigma_range=(0.01, 0.06))
+    errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, bg, seed=7, label=f"bg {bg}")
+    assert bad.sum() <= 2
+    assert not errs, errs
+    # (the scene does clamp: a forward of it has saturated pixels)
+    m = pkg.synthetic.to_model(sc, pkg.GaussianModel, cuda)
+    with torch.no_grad():
+        img = pkg.GaussianRenderer().render(Cam(W, H, sc.fovx, sc.fovy), m,
+                                            pkg.RenderSettings(H, W, torch.tensor(bg)))["image"]
+    assert int((img[0] == 1.0).sum()) > 100
+
+
 @pytest.mark.parametrize("wh", [(1, 1), (5, 3), (17, 1), (1, 33), (129, 65)])
 def test_odd_image_sizes_vs_oracle(pkg, cuda, wh):
     """Images of one pixel, one row, one column, and sizes just past a tile
