@@ -28,6 +28,9 @@ constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
+#ifndef GS_RANGES_X4
+#define GS_RANGES_X4 1
+#endif
 #ifndef GS_SORT_IPT
 #define GS_SORT_IPT 8
 #endif
@@ -1140,6 +1143,49 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
 // (no memset): position p in [0, T] is a boundary when key[p-1] != key[p]
 // (key[-1] = -1, key[T] = num_tiles); it closes the previous tile, opens the
 // next and writes the tiles in between as empty at p.
+// Four consecutive positions per thread (the default tile's four-cell slot
+// flags): one 16-B key load, the previous key from the neighbouring lane, one
+// 16-B flag store.  Same writes as k_tile_ranges.
+__global__ __launch_bounds__(kBlock) void k_tile_ranges4(gs_range_args a) {
+  const long long p0 = 4 * ((long long)blockIdx.x * kBlock + threadIdx.x);
+  const long long T = a.num_pairs;
+  if (p0 > T) return;
+  const int lane = threadIdx.x & 63;
+  uint4 k = make_uint4(0u, 0u, 0u, 0u);
+  if (p0 + 3 < T) {
+    k = reinterpret_cast<const uint4 *>(a.sorted_keys)[p0 / 4];
+  } else {
+    if (p0 < T) k.x = a.sorted_keys[p0];
+    if (p0 + 1 < T) k.y = a.sorted_keys[p0 + 1];
+    if (p0 + 2 < T) k.z = a.sorted_keys[p0 + 2];
+  }
+  // the key before p0: the previous lane's last one (its positions end at p0 - 1)
+  uint32_t before = (uint32_t)__shfl_up((int)k.w, 1, 64);
+  if (lane == 0) before = p0 > 0 ? a.sorted_keys[p0 - 1] : 0u;
+  if (a.slot_live) {
+    if (p0 + 3 < T)
+      reinterpret_cast<uint4 *>(a.slot_live)[p0 / 4] = make_uint4(0u, 0u, 0u, 0u);
+    else
+      for (long long q = p0; q < T; ++q) reinterpret_cast<uint32_t *>(a.slot_live)[q] = 0u;
+  }
+  const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long p = p0 + i;
+    const bool in = p <= T;  // (lanes past the end take part in the wave fills with nothing to fill)
+    const long long prev = !in ? 0 : (p > 0 ? (long long)(i ? kk[i - 1] : before) : -1);
+    const long long cur = !in ? 0 : (p < T ? (long long)kk[i] : (long long)a.num_tiles);
+    const bool edge = in && cur != prev;
+    if (edge && prev >= 0) a.ranges[2 * prev + 1] = (uint32_t)p;
+    if (edge && cur < a.num_tiles) a.ranges[2 * cur] = (uint32_t)p;
+    const uint32_t t0 = (uint32_t)(prev + 1), t1 = edge ? (uint32_t)cur : t0;
+    const bool wide = edge && t1 > t0 + kWaveFillRun;
+    if (edge && !wide)
+      for (uint32_t t = t0; t < t1; ++t) a.ranges[2 * t] = a.ranges[2 * t + 1] = (uint32_t)p;
+    wave_fill_runs(wide, t0, t1, (uint32_t)p, [&](uint32_t t, uint32_t q) { a.ranges[2 * t] = a.ranges[2 * t + 1] = q; });
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
   const long long p = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (p > a.num_pairs) return;
@@ -2494,7 +2540,13 @@ gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream) {
   if (a->num_pairs > 0 && !a->sorted_keys) return fail(GS_ERR_INVALID_ARG, "%s: null buffer", "gs_tile_ranges");
   if (a->slot_live && (a->cells < 1 || (a->cells == 4 && (reinterpret_cast<uintptr_t>(a->slot_live) & 3u))))
     return fail(GS_ERR_INVALID_ARG, "%s: slot_live needs cells >= 1 (4-B aligned at 4 cells)", "gs_tile_ranges");
-  k_tile_ranges<<<div_up(a->num_pairs + 1, kBlock), kBlock, 0, s>>>(*a);
+  // four positions per thread where the flags are 4-B words (the default
+  // tile) and the keys 16-B aligned
+  if (GS_RANGES_X4 && (!a->slot_live || a->cells == 4) && (reinterpret_cast<uintptr_t>(a->sorted_keys) & 15u) == 0 &&
+      (reinterpret_cast<uintptr_t>(a->slot_live) & 15u) == 0)
+    k_tile_ranges4<<<div_up(a->num_pairs / 4 + 1, kBlock), kBlock, 0, s>>>(*a);
+  else
+    k_tile_ranges<<<div_up(a->num_pairs + 1, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_tile_ranges");
 }
 
