@@ -1012,6 +1012,9 @@ constexpr uint32_t kOwnerCap = kBlock * 64;
 #define GS_HIST_SPAN 8
 #endif
 constexpr int kHistSpan = GS_HIST_SPAN;
+// kHist: the fused first-pass histogram (GS_EMIT_TILE_HIST, off); the product
+// instantiation carries neither its LDS table nor its registers
+template <bool kHist>
 __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32_t *partials, TileHist th) {
   __shared__ uint32_t s_off[kBlock + 1];
   __shared__ uint32_t s_g[kBlock];
@@ -1019,7 +1022,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   __shared__ uint32_t s_tmp[4];
   __shared__ uint32_t s_tmp3[3][kBlock / kWave];
   __shared__ uint8_t s_owner[kOwnerCap];
-  __shared__ uint32_t s_hist[kHistSpan * kRadix];
+  __shared__ uint32_t s_hist[kHist ? kHistSpan * kRadix : 1];
   // T entries do not fit: do nothing (the caller re-emits into T-sized
   // buffers; the slot pass below is not idempotent, so it must run once)
   const uint32_t T = a.counters[1];
@@ -1028,7 +1031,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   uint32_t out_base = partials[blockIdx.x];
   // first-pass digit counts of the entries this block writes: sort block
   // (out_base + o) / kSortChunk, digit key & hmask (shift 0)
-  const bool hist = th.bits > 0;
+  const bool hist = kHist && th.bits > 0;
   const uint32_t hmask = (1u << th.bits) - 1u, nbs = (T + kSortChunk - 1) / kSortChunk;
   const uint32_t hb0 = out_base / kSortChunk;
   if (hist) {
@@ -1871,8 +1874,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
 // then the lane sums are added in a fixed DPP order -- bitwise reproducible.
 // The q lanes of a slot read its partial record together, and consecutive
 // Gaussians' slots are adjacent (index-order slots): coalesced.  Flags of up
-// to 4 slots are loaded at once, then their partials: two round trips per
-// 4 HL slots of g (the mean is 4.4 on C3).  Partials are 40 B, 8-B aligned:
+// to kGatherNB slots are loaded at once, then their partials: two round trips
+// per kGatherNB x HL slots of g (the mean is 4.4 on C3).  Partials are 40 B, 8-B aligned:
 // read as float2.
 __device__ __forceinline__ float quad_sum(float v) {
   v += dpp_row<0xB1>(v);  // quad_perm [1,0,3,2]
@@ -1898,6 +1901,13 @@ constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
 
 // Gaussian g's partials summed by its QL x HL lanes (lane (h, q) of g at
 // t % LPG); every one of the LPG lanes returns the sum in acc.
+// Slots per lane per round trip: 3 (56 VGPRs, 8 waves per SIMD) against 4
+// (71, 7 waves): 110.9 -> 105.9 us at C3 (profiles/r05/gather_nb_ab/); the
+// lane's slot order, and so every sum, is the same for any batch size.
+#ifndef GS_GATHER_NB
+#define GS_GATHER_NB 3
+#endif
+constexpr int kGatherNB = GS_GATHER_NB;
 template <int QL, int HL, int kNG>
 __device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint32_t ng, long long t, float2 acc[kF2]) {
   constexpr int LPG = QL * HL;
@@ -1922,28 +1932,28 @@ __device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint3
     const uint8_t *flag = a.slot_live + off * ng + qc;  // (slot e, group qc) at flag[ng e]
     // group-qc partial of slot e at part + e * ng * GS_PARTIAL_STRIDE (dense 40-B records)
     const float2 *part = reinterpret_cast<const float2 *>(a.pair_grads + (off * ng + qc) * GS_PARTIAL_STRIDE);
-    for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += 4 * HL) {
-      // the 4 flags in one round trip: unconditional loads (past the end
+    for (uint32_t e0 = (uint32_t)h; e0 < cnt; e0 += kGatherNB * HL) {
+      // the batch's flags in one round trip: unconditional loads (past the end
       // the clamped index re-reads slot e0), masked after
-      uint32_t f[4];
+      uint32_t f[kGatherNB];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < kGatherNB; ++i) {
         const uint32_t e = e0 + HL * i;
         f[i] = flag[(size_t)ng * (e < cnt ? e : e0)];
       }
-      // all four flags tested before any partial is requested: the partial
+      // all the batch's flags tested before any partial is requested: the partial
       // loads are conditional, so a wait for a later flag placed between them
       // would have to count them out conservatively and drain them
       uint32_t fm = 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fm |= (e0 + HL * i < cnt && f[i]) ? 1u << i : 0u;
+      for (int i = 0; i < kGatherNB; ++i) fm |= (e0 + HL * i < cnt && f[i]) ? 1u << i : 0u;
       asm volatile("" : "+v"(fm));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) f[i] = (fm >> i) & 1u;
-      f4_u8 va[4], vb[4];
-      f2_u8 vc[4];
+      for (int i = 0; i < kGatherNB; ++i) f[i] = (fm >> i) & 1u;
+      f4_u8 va[kGatherNB], vb[kGatherNB];
+      f2_u8 vc[kGatherNB];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < kGatherNB; ++i) {
         const float *src = reinterpret_cast<const float *>(part + (size_t)(e0 + HL * i) * ng * kF2);
         // (non-temporal loads, for data read once, measured +10 us: profiles/r03/experiments.md)
         va[i] = f[i] ? *reinterpret_cast<const f4_u8 *>(src) : f4_u8{0.f, 0.f, 0.f, 0.f};
@@ -1951,7 +1961,7 @@ __device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint3
         vc[i] = f[i] ? *reinterpret_cast<const f2_u8 *>(src + 8) : f2_u8{0.f, 0.f};
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < kGatherNB; ++i) {
         if (!f[i]) continue;
         acc[0].x += va[i].x; acc[0].y += va[i].y; acc[1].x += va[i].z; acc[1].y += va[i].w;
         acc[2].x += vb[i].x; acc[2].y += vb[i].y; acc[3].x += vb[i].z; acc[3].y += vb[i].w;
@@ -2468,7 +2478,7 @@ gs_status gs_internal_bin_emit_hist(const gs_bin_args *a, uint32_t *tile_counts,
     return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_internal_bin_emit_hist");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
-  k_bin_emit<<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace, TileHist{tile_counts, 0u, bits});
+  k_bin_emit<true><<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace, TileHist{tile_counts, 0u, bits});
   return check_launch("gs_bin_emit");
 }
 
@@ -2528,7 +2538,7 @@ gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream) {
   if (a->capacity < 0) return fail(GS_ERR_INVALID_ARG, "%s: negative capacity", "gs_bin_emit");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (int)div_up(a->n, kBinChunk);
-  k_bin_emit<<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace, TileHist{nullptr, 0u, 0});
+  k_bin_emit<false><<<nb, kBlock, 0, s>>>(*a, (const uint32_t *)a->workspace, TileHist{nullptr, 0u, 0});
   return check_launch("gs_bin_emit");
 }
 
