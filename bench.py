@@ -89,6 +89,9 @@ def parse():
                     help="nccl (= RCCL over xGMI) for the driver; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--force-dist", action="store_true",
                     help="init the process group and all-reduce even at world size 1 (rehearses the RCCL path)")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="replay the step as one HIP graph over a device-resident frame (graph_step.GraphedStep; "
+                         "auto: at world size 1 with the optimizer) or run it eagerly through autograd")
     a = ap.parse_args()
     n0, w0, h0 = CONFIGS[a.config]
     a.gaussians = n0 if a.gaussians is None else a.gaussians
@@ -213,7 +216,7 @@ def main():
         for p in params:
             opt.set_output(p, torch.empty_like(p))
 
-    def step():
+    def eager_step():
         if opt is not None:
             opt.zero_grad(set_to_none=True)
         else:
@@ -221,7 +224,7 @@ def main():
                 p.grad = None
         out = renderer.render(cam, model, settings)
         torch.autograd.backward([out["image"], out["alpha"], out["depth"]], cot)
-        if step.no_collective:  # (collective_share's reference run)
+        if eager_step.no_collective:  # (collective_share's reference run)
             if opt is not None:
                 opt.step()
         elif reducer is not None and opt is not None:
@@ -232,7 +235,19 @@ def main():
             opt.step()
         frames.append(out)
 
-    step.no_collective = False
+    eager_step.no_collective = False
+    # The step replayed as one HIP graph: the same kernels
+    # on the same buffers, no per-frame host read-back, one launch per step;
+    # a frame that fails on the device is skipped by Adam and redone eagerly
+    # (gstep.redone).  World size 1: the collective stays eager at N > 1.
+    use_graph = a.graph == "on" or (a.graph == "auto" and reducer is None and opt is not None)
+    gstep = None
+    if use_graph:
+        gstep = pkg.GraphedStep(renderer, cam, model, settings, cot, opt, eager_step=eager_step)
+        torch.cuda.set_stream(gstep.stream)  # (every step, eager or replayed, on the graph's queue)
+        step = gstep.step
+    else:
+        step = eager_step
     for _ in range(a.spinup_steps + a.warmup):
         step()
         frames.clear()
@@ -245,6 +260,10 @@ def main():
     # diagnostic steps after it, whose events would stall the launch chain.
     StageTimer.enabled, StageTimer.only = True, {"blend_bwd", "project_bwd"}
     StageTimer.reset()
+    if gstep is not None:
+        gstep.finish()
+        gstep.timing, gstep.event_pairs = True, []  # (event record nodes re-pointed per replay)
+        redone0 = sum(k for _, k in gstep.redone)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
@@ -253,7 +272,19 @@ def main():
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
-    bwd_live = StageTimer.durations_ms().get("blend_bwd", [])
+    if gstep is not None:
+        gstep.finish()  # (checks the last replay; a redo would show in graph_info below)
+        gstep.timing = False
+        bwd_live = gstep.blend_backward_ms()
+        graph_info = {"replayed": True, "nodes": gstep.graph.num_nodes if gstep.graph else None,
+                      "steps_redone_in_timed_region": sum(k for _, k in gstep.redone) - redone0,
+                      "redone": gstep.redone, "disabled": gstep.disabled,
+                      "capacity": gstep._cap, "depth_window_bits": (gstep.window_used or (0, 32))[1],
+                      "note": "render fwd + bwd + FusedAdam captured once (hipStreamBeginCapture) over a "
+                              "device-resident frame and replayed with hipGraphLaunch; no host read-back"}
+    else:
+        bwd_live = StageTimer.durations_ms().get("blend_bwd", [])
+        graph_info = {"replayed": False}
     dt = t1 - t0
     if dist is not None:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -261,13 +292,13 @@ def main():
         dt = float(t.item())
     StageTimer.only = None
     StageTimer.reset()
-    coll = collective_share(a, dist, dev, reducer, model, step, frames, dt) if reducer is not None else None
+    coll = collective_share(a, dist, dev, reducer, model, eager_step, frames, dt) if reducer is not None else None
     # the per-stage breakdown from the stage-by-stage path (the same kernels;
     # the frame entry points would time only the blend backward)
     from mini3dgs_amd import rasterizer as _RZ
     frame_calls, _RZ._FRAME_CALLS = _RZ._FRAME_CALLS, False
     for _ in range(a.diag_steps):
-        step()
+        eager_step()
         frames = frames[-1:]
     _RZ._FRAME_CALLS = frame_calls
     stages = {k: sum(v) / len(v) for k, v in StageTimer.durations_ms().items()}
@@ -286,9 +317,17 @@ def main():
         camp = pkg.camera_params(cam, settings)
         pair_counts = torch.empty((H * W,), dtype=torch.int32, device=dev)
         pix_neval = torch.empty((H * W,), dtype=torch.int32, device=dev)
-        _, _, _, _, _, _, _, fr = RZ.forward_pipeline(
-            camp, model._xyz, None, model._scaling, model._rotation, model._features_dc[:, 0, :],
-            torch.sigmoid(model._opacity).squeeze(1), pair_counts=pair_counts, pix_neval=pix_neval)
+        with torch.no_grad():
+            op = torch.sigmoid(model._opacity).squeeze(1)
+            img, al, dp, m2, cn, _, _, fr = RZ.forward_pipeline(
+                camp, model._xyz, None, model._scaling, model._rotation, model._features_dc[:, 0, :], op,
+                pair_counts=pair_counts, pix_neval=pix_neval, need_grad=True)
+            # and its backward, for L: the live (entry, cell) pairs -- the partials
+            # the blend backward writes and the gather reads (its slot flags)
+            RZ.backward_pipeline(camp, fr, model._xyz, None, model._scaling, model._rotation,
+                                 model._features_dc[:, 0, :], op, m2, cn, cot[0], cot[1], cot[2], None, None,
+                                 outputs=(img, al, dp))
+            live_pairs = int(fr.slot_live.count_nonzero())
         R, E, Cc = algorithmic_counts(pix_neval, pair_counts, H, W, tiles_x, tiles_y)
         M, T = fr.M, fr.T
         num_tiles = tiles_x * tiles_y
@@ -354,7 +393,9 @@ def main():
                        "preset": wl,
                        "gaussians": n, "width": W, "height": H, "views_per_step": world,
                        "parallelism": f"dp{world} (one view per GPU)", "visible": M, "tile_touches": T,
-                       "records_consumed": R, "evaluated_pairs": E, "contributing_pairs": Cc},
+                       "records_consumed": R, "evaluated_pairs": E, "contributing_pairs": Cc,
+                       "live_entry_cells": live_pairs},
+            "graph": graph_info,
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
             "stages_note": f"HIP-event intervals from {a.diag_steps} diagnostic steps after the timed region, "
                            "run stage by stage (GS_FRAME_CALLS=0 path: the same kernels as the timed steps' frame "
@@ -366,7 +407,10 @@ def main():
             "psnr_vs_ref": psnr,
         }
         if reducer is not None:
-            nsteps = a.spinup_steps + a.warmup + 3 * a.steps + a.diag_steps
+            # steps that issued collectives: spin-up, warm-up, the timed steps,
+            # collective_share's timing run (its no-collective run issues none)
+            # and the diagnostic steps
+            nsteps = a.spinup_steps + a.warmup + 2 * a.steps + a.diag_steps
             line["allreduce"] = {"ranges_per_step": reducer.overlap_chunks(), "pipelined_adam": opt is not None,
                                  "host_us_per_step": {k: round(1e6 * v / nsteps, 1) for k, v in reducer.host_s.items()},
                                  "avg": reducer._avg, "native": reducer.native_status["native"],

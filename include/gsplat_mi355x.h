@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 20
+#define GS_ABI_VERSION 21
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
 #define GS_MAX_TILE 4096      /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
                                  of at least max(W, H) renders the same as any larger one (one tile
@@ -47,8 +47,17 @@ extern "C" {
 #define GS_RECORD_FLOATS 12   /* per-Gaussian splat record (3 x float4), see DESIGN.md */
 #define GS_PAIR_GRAD_FLOATS 10 /* per (list entry, partial group) gradient partial (gs_partial_groups) */
 #define GS_PARTIAL_STRIDE 10   /* floats between partials in pair_grads (dense: 40 B each) */
-#define GS_NUM_COUNTERS 4     /* [0] visible M, [1] tile touches T, [2] / [3] min / max fp32 bits of the
-                                 visible depths (0xFFFFFFFF / 0 when none; see gs_project_args) */
+#define GS_NUM_COUNTERS 8     /* [0] visible M, [1] tile touches T, [2] / [3] min / max fp32 bits of the
+                                 visible depths (0xFFFFFFFF / 0 when none; see gs_project_args),
+                                 [4] the frame status (GS_FRAME_* bits below), [5] the list entries the
+                                 later stages use: T, or 0 when the status is non-zero; [6..7] unused */
+/* Frame status bits (gs_bin_count, counters[4]): what a device-resident frame
+ * (gs_render_fwd_args.device_counts) could not do on the device.  A frame
+ * with a non-zero status is drawn with empty tile lists (memory-safe, not
+ * the reference's image) and its caller renders it again on the host path. */
+#define GS_FRAME_NEED_CAPACITY 1u /* T > the tile workspace's capacity */
+#define GS_FRAME_WINDOW_MISS 2u   /* a visible depth left the depth-key window (or an MSD bucket overflowed) */
+#define GS_FRAME_EMPTY 4u         /* M == 0: renderer.py:74-83's background image is the host's */
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -207,13 +216,25 @@ typedef struct gs_bin_args {
   int64_t capacity;      /* entries tile_keys / pair_gauss hold.  gs_bin_emit does nothing
                             when T = counters[1] > capacity, so it may be queued before T is
                             read back (then emit again into buffers of >= T entries) */
-  uint32_t *host_counters; /* optional [5]: the device address of pinned host memory
+  uint32_t *host_counters; /* optional [8]: the device address of pinned host memory
                               (hipHostGetDevicePointer) that gs_bin_count also writes
                               counters[0..3] to, then -- after a system-scope fence --
                               host_seq to [4]: the caller polls [4] for the value it passed
                               and reads (M, T) with no copy and no event in the stream.
                               NULL: counters only */
   uint32_t host_seq;
+  /* The frame status (counters[4], GS_FRAME_*), formed by gs_bin_count from
+   * (M, T, the depth range) against capacity and the depth-key window the
+   * keys were cut to (gs_project_args.key_base / key_bits): */
+  uint32_t key_base;
+  int32_t key_bits;        /* 0: no window check */
+  uint32_t *step_flags;    /* optional device word: the status is ORed into it (sticky until the caller
+                              clears it; gs_adam_args.skip_flag reads it) */
+  uint32_t *frame_seq;     /* optional device word: incremented by every gs_bin_count; its new value is
+                              written to host_counters[4] in place of host_seq (a captured graph
+                              replays one frame per value).  host_counters also gets [5] the status,
+                              [6] the step flags after this frame (the status without step_flags) and,
+                              when this frame is the first to set them, [7] its sequence value */
 } gs_bin_args;
 gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream);
 gs_status gs_bin_emit(const gs_bin_args *a, gs_stream_t stream);
@@ -228,6 +249,9 @@ typedef struct gs_range_args {
   uint8_t *slot_live;          /* optional (NULL: none): zeroed here, [T, cells] -- the backward's
                                   gs_blend_bwd_args.slot_live, cleared without a kernel of its own */
   int32_t cells;               /* gs_partial_groups(tile_size), with slot_live */
+  const uint32_t *num_pairs_dev; /* optional device word (counters[5]): the entries are
+                                  min(*num_pairs_dev, num_pairs), num_pairs only bounding them (a
+                                  launch sized by capacity before T is known on the host) */
 } gs_range_args;
 gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream);
 
@@ -371,6 +395,8 @@ typedef struct gs_project_bwd_args {
   float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS]: g's partials summed (written first when
                                   pair_grads is given, else read as is); NULL: no blend gradient */
   int32_t partial_groups;      /* G of pair_grads / slot_live: the blend backward's cell_count */
+  const uint32_t *frame_status; /* optional device word (counters[4]): non-zero -> the gather writes
+                                  zero sums (a device-resident frame that failed reads no partials) */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
 /* The gather alone: grad_sums[g] = (accumulate ? grad_sums[g] : 0) + the sum
@@ -404,6 +430,17 @@ typedef struct gs_adam_args {
   int32_t num_tensors;
   float beta1, beta2, eps;
   gs_adam_tensor t[GS_ADAM_MAX_TENSORS];
+  /* Replayed steps (a captured graph whose kernel arguments are fixed):
+   * skip_flag: optional device word -- non-zero: the launch updates nothing
+   *   (gs_bin_args.step_flags: the frame of this step failed on the device
+   *   and the caller redoes the step on the host path);
+   * hyper / hyper_row: optional -- tensor i's lr, bias_correction1 and
+   *   bias_correction2_sqrt are read from hyper[(r * GS_ADAM_MAX_TENSORS + i)
+   *   * 3 + 0..2], r = *hyper_row (a device word, e.g. gs_bin_args.frame_seq),
+   *   instead of t[i]; the caller fills the rows the replays will reach. */
+  const uint32_t *skip_flag;
+  const float *hyper;
+  const uint32_t *hyper_row;
 } gs_adam_args;
 gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream);
 
@@ -522,6 +559,18 @@ typedef struct gs_render_fwd_args {
   uint32_t *pair_counts;           /* optional, gs_blend_fwd_args.pair_counts */
   uint32_t *pix_neval;             /* optional, gs_blend_fwd_args.pix_neval */
   int32_t resume;                  /* 1: continue after GS_NEED_CAPACITY, with a tile workspace of >= T */
+  int32_t poll_timeout_ms;         /* the counter poll's patience before it synchronises the stream and
+                                      looks once more (0: 10 s) */
+  /* Device-resident frame (device_counts = 1): no host read-back at all.  The
+   * count's status (GS_FRAME_*) and T stay on the device: the tile sort, the
+   * ranges and the blend are launched for `capacity` entries (needs a tile
+   * workspace) and read T themselves; a failed frame is drawn with empty
+   * lists and flagged in counters[4] (and *step_flags).  The call returns
+   * GS_OK with M, T unknown; the host reads (M, T, depth range, seq, status)
+   * from the pinned counters whenever it likes.  For graph capture. */
+  int32_t device_counts;
+  uint32_t *step_flags;            /* optional, gs_bin_args.step_flags */
+  uint32_t *frame_seq;             /* optional, gs_bin_args.frame_seq */
   /* results (and state for resume / the backward) */
   int32_t M, T;
   uint32_t depth_min_bits, depth_max_bits; /* counters[2..3] */
@@ -549,6 +598,8 @@ typedef struct gs_render_bwd_args {
                                       caller's own gs_project_backward, e.g. per row range) */
   void *blend_events[2];           /* optional hipEvent_t pair, recorded on the stream right before and
                                       after the blend backward launch(es): its time alone (profiling) */
+  int32_t device_counts;           /* the forward was device-resident: M, T are not read; pair_grads holds
+                                      capacity * flag_groups partials; the gather reads the frame status */
 } gs_render_bwd_args;
 gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream);
 /* Byte offsets of the buffers inside the two workspaces (for diagnostics and

@@ -13,9 +13,10 @@ from .loss import SSIMLoss, GaussianLoss, photometric_loss  # noqa: F401
 from .config import TrainingConfig, ConfigManager  # noqa: F401
 from .dataset import CameraDataset, NeRFSyntheticDataset, COLMAPDataset, load_dataset  # noqa: F401
 from .trainer import GaussianTrainer  # noqa: F401
-from . import _native, synthetic, distributed, optim, loss, dataset, trainer  # noqa: F401
+from .graph_step import GraphedStep  # noqa: F401
+from . import _native, synthetic, distributed, optim, loss, dataset, trainer, graph_step  # noqa: F401
 
 __all__ = ["GaussianRenderer", "RenderSettings", "GaussianModel", "Camera", "CameraUtils",
            "CameraParams", "rasterize", "camera_params", "SSIMLoss", "GaussianLoss", "photometric_loss",
            "TrainingConfig", "ConfigManager", "CameraDataset", "NeRFSyntheticDataset", "COLMAPDataset",
-           "load_dataset", "GaussianTrainer"]
+           "load_dataset", "GaussianTrainer", "GraphedStep"]

@@ -26,8 +26,11 @@ GS_QUAD = 8  # 8x8 pixel cells per wave, ceil(tile/8)^2 per tile (gs_tile_quads)
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10
 GS_PARTIAL_STRIDE = 10  # floats between partials in pair_grads (dense; gs_partial_groups per entry)
-GS_NUM_COUNTERS = 4
-GS_ABI_VERSION = 20
+GS_NUM_COUNTERS = 8  # M, T, depth-bits min / max, frame status, T_eff (GS_NUM_COUNTERS in the header)
+GS_ABI_VERSION = 21
+# frame status bits (counters[4]; the pinned counters' [5]): what a device-resident
+# frame could not do on the device, so its step is redone on the host path
+GS_FRAME_NEED_CAPACITY, GS_FRAME_WINDOW_MISS, GS_FRAME_EMPTY = 1, 2, 4
 GS_NEED_CAPACITY, GS_RETRY_FULL_KEYS = 4, 5  # gs_render_forward: what to do next (not errors)
 GS_SH_REST = 15  # [15,3] rest coefficients per Gaussian (degree <= 3)
 
@@ -67,13 +70,14 @@ class GsBinArgs(C.Structure):
         ("workspace_bytes", C.c_size_t),
         ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp), ("records", _vp),
         ("capacity", C.c_int64), ("host_counters", _vp), ("host_seq", C.c_uint32),
+        ("key_base", C.c_uint32), ("key_bits", C.c_int32), ("step_flags", _vp), ("frame_seq", _vp),
     ]
 
 
 class GsRangeArgs(C.Structure):
     _fields_ = [
         ("num_pairs", C.c_int32), ("num_tiles", C.c_int32), ("sorted_keys", _vp), ("ranges", _vp),
-        ("slot_live", _vp), ("cells", C.c_int32),
+        ("slot_live", _vp), ("cells", C.c_int32), ("num_pairs_dev", _vp),
     ]
 
 
@@ -102,7 +106,7 @@ class GsProjectBwdArgs(C.Structure):
         ("rects", _vp), ("pair_offset", _vp), ("order", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
         ("g_conics", _vp), ("d_xyz", _vp), ("d_cov3d", _vp), ("d_scaling", _vp),
         ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
-        ("slot_live", _vp), ("grad_sums", _vp), ("partial_groups", C.c_int32),
+        ("slot_live", _vp), ("grad_sums", _vp), ("partial_groups", C.c_int32), ("frame_status", _vp),
     ]
 
 
@@ -119,8 +123,10 @@ class GsRenderFwdArgs(C.Structure):
         ("image", _vp), ("alpha", _vp), ("depth", _vp), ("fb", GsFrameBuffers), ("key_base", C.c_uint32),
         ("key_bits", C.c_int32), ("depth_sort_msd", C.c_int32), ("zero_slot_flags", C.c_int32),
         ("host_counters_dev", _vp), ("host_counters_host", _vp), ("host_seq", C.c_uint32), ("pair_counts", _vp),
-        ("pix_neval", _vp), ("resume", C.c_int32), ("M", C.c_int32), ("T", C.c_int32), ("depth_min_bits", C.c_uint32),
-        ("depth_max_bits", C.c_uint32), ("depth_alt", C.c_int32), ("tile_alt", C.c_int32),
+        ("pix_neval", _vp), ("resume", C.c_int32), ("poll_timeout_ms", C.c_int32), ("device_counts", C.c_int32),
+        ("step_flags", _vp), ("frame_seq", _vp), ("M", C.c_int32), ("T", C.c_int32),
+        ("depth_min_bits", C.c_uint32), ("depth_max_bits", C.c_uint32), ("depth_alt", C.c_int32),
+        ("tile_alt", C.c_int32),
     ]
 
 
@@ -131,7 +137,7 @@ class GsRenderBwdArgs(C.Structure):
         ("alpha", _vp), ("depth", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp), ("g_means2d", _vp), ("g_conics", _vp), ("pair_grads", _vp),
         ("flags_zeroed", C.c_int32), ("project", C.c_int32), ("d_xyz", _vp), ("d_cov3d", _vp),
         ("d_scaling", _vp), ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
-        ("grad_sums", _vp), ("blend_events", _vp * 2),
+        ("grad_sums", _vp), ("blend_events", _vp * 2), ("device_counts", C.c_int32),
     ]
 
 
@@ -149,7 +155,7 @@ class GsAdamTensor(C.Structure):
 class GsAdamArgs(C.Structure):
     _fields_ = [
         ("num_tensors", C.c_int32), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
-        ("t", GsAdamTensor * GS_ADAM_MAX_TENSORS),
+        ("t", GsAdamTensor * GS_ADAM_MAX_TENSORS), ("skip_flag", _vp), ("hyper", _vp), ("hyper_row", _vp),
     ]
 
 
@@ -316,7 +322,87 @@ def _hip():
         _HIP.hipEventCreate.restype = C.c_int
         _HIP.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), _vp, _vp]
         _HIP.hipEventElapsedTime.restype = C.c_int
+        for name, args in (("hipStreamBeginCapture", [_vp, C.c_int]), ("hipStreamEndCapture", [_vp, C.POINTER(_vp)]),
+                           ("hipGraphInstantiate", [C.POINTER(_vp), _vp, _vp, _vp, C.c_size_t]),
+                           ("hipGraphLaunch", [_vp, _vp]), ("hipGraphExecDestroy", [_vp]),
+                           ("hipGraphDestroy", [_vp]), ("hipGraphGetNodes", [_vp, _vp, C.POINTER(C.c_size_t)]),
+                           ("hipGraphNodeGetType", [_vp, C.POINTER(C.c_int)]),
+                           ("hipGraphEventRecordNodeGetEvent", [_vp, C.POINTER(_vp)]),
+                           ("hipGraphExecEventRecordNodeSetEvent", [_vp, _vp, _vp]),
+                           ("hipEventDestroy", [_vp]), ("hipGetErrorString", [C.c_int])):
+            f = getattr(_HIP, name)
+            f.argtypes = args
+            f.restype = C.c_int
+        _HIP.hipGetErrorString.restype = C.c_char_p
     return _HIP
+
+
+def _hip_check(err: int, what: str) -> None:
+    if err != 0:
+        raise RuntimeError(f"{what} failed: {_hip().hipGetErrorString(err).decode(errors='replace')}")
+
+
+_HIP_GRAPH_NODE_EVENT_RECORD = 7  # hipGraphNodeTypeEventRecord
+_HIP_CAPTURE_THREAD_LOCAL = 1     # hipStreamCaptureModeThreadLocal
+
+
+class HipGraph:
+    """A HIP graph captured from the work one callable enqueues on `stream`
+    (hipStreamBeginCapture / EndCapture / GraphInstantiate on the HIP runtime
+    torch loaded), replayed with hipGraphLaunch.  The callable must not
+    allocate or synchronise: every buffer it names is the caller's and stays
+    where it is for the graph's life.  Event records the library makes during
+    the capture become event record nodes (gs_render_bwd_args.blend_events);
+    set_event_pair() points them at fresh events before a replay, so that
+    each replay's interval can be read afterwards."""
+
+    def __init__(self, stream: int, enqueue):
+        if not stream:
+            raise ValueError("HipGraph needs a non-default stream (the null stream cannot be captured)")
+        h = _hip()
+        self.stream, self.graph, self.exec = stream, _vp(), _vp()
+        _hip_check(h.hipStreamBeginCapture(_vp(stream), _HIP_CAPTURE_THREAD_LOCAL), "hipStreamBeginCapture")
+        try:
+            enqueue()
+        finally:
+            err = h.hipStreamEndCapture(_vp(stream), C.byref(self.graph))
+        _hip_check(err, "hipStreamEndCapture")
+        _hip_check(h.hipGraphInstantiate(C.byref(self.exec), self.graph, None, None, 0), "hipGraphInstantiate")
+        cnt = C.c_size_t(0)
+        _hip_check(h.hipGraphGetNodes(self.graph, None, C.byref(cnt)), "hipGraphGetNodes")
+        nodes = (_vp * max(cnt.value, 1))()
+        _hip_check(h.hipGraphGetNodes(self.graph, nodes, C.byref(cnt)), "hipGraphGetNodes")
+        self.num_nodes = cnt.value
+        self.event_nodes = {}  # event handle recorded at capture -> its node
+        for i in range(cnt.value):
+            t = C.c_int(-1)
+            _hip_check(h.hipGraphNodeGetType(nodes[i], C.byref(t)), "hipGraphNodeGetType")
+            if t.value == _HIP_GRAPH_NODE_EVENT_RECORD:
+                ev = _vp()
+                _hip_check(h.hipGraphEventRecordNodeGetEvent(nodes[i], C.byref(ev)), "hipGraphEventRecordNodeGetEvent")
+                self.event_nodes[ev.value] = _vp(nodes[i])
+
+    def set_event(self, captured_event: int, event: int) -> None:
+        """The node that records `captured_event` records `event` from the next replay on."""
+        _hip_check(_hip().hipGraphExecEventRecordNodeSetEvent(self.exec, self.event_nodes[captured_event],
+                                                              _vp(event)), "hipGraphExecEventRecordNodeSetEvent")
+
+    def launch(self) -> None:
+        _hip_check(_hip().hipGraphLaunch(self.exec, _vp(self.stream)), "hipGraphLaunch")
+
+    def close(self) -> None:
+        if self.exec:
+            _hip().hipGraphExecDestroy(self.exec)
+            self.exec = _vp()
+        if self.graph:
+            _hip().hipGraphDestroy(self.graph)
+            self.graph = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class RawEvent:

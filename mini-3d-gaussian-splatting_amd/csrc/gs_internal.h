@@ -19,7 +19,7 @@ __attribute__((visibility("hidden"))) gs_status gs_internal_check_launch(const c
 __attribute__((visibility("hidden"))) gs_status gs_internal_radix_sort_pairs(
     uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt, int32_t n, int32_t begin_bit,
     int32_t end_bit, int32_t vals_are_iota, void *workspace, size_t workspace_bytes, int32_t *result_in_alt,
-    int32_t first_counts_ready, gs_stream_t stream);
+    int32_t first_counts_ready, const uint32_t *n_dev, gs_stream_t stream);
 // the digit width of gs_radix_sort_pairs' first pass over bits [begin_bit, end_bit)
 __attribute__((visibility("hidden"))) int32_t gs_internal_first_pass_bits(int32_t begin_bit, int32_t end_bit);
 // gs_bin_count, also clearing the tile sort's first-pass count table of a
@@ -39,4 +39,5 @@ __attribute__((visibility("hidden"))) gs_status gs_internal_bin_emit_hist(const 
 __attribute__((visibility("hidden"))) int32_t gs_internal_small_sort_max(void);
 __attribute__((visibility("hidden"))) gs_status gs_internal_small_sort(const uint32_t *keys, const uint32_t *vals,
                                                                       uint32_t *keys_out, uint32_t *vals_out,
-                                                                      int32_t n, int32_t bits, gs_stream_t stream);
+                                                                      int32_t n, int32_t bits, const uint32_t *n_dev,
+                                                                      gs_stream_t stream);

@@ -12,6 +12,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdio.h>
+
 #include <chrono>
 
 #include "gs_internal.h"
@@ -102,6 +104,35 @@ bool window_holds(uint32_t key_base, int32_t key_bits, uint32_t zmin, uint32_t z
   return zmin >= key_base && (uint64_t)(zmax - key_base) < lim;
 }
 
+// An event record on `stream`; inside a stream capture it becomes an event
+// record node of the graph (hipEventRecordExternal), so that every replay
+// records it -- the timing events of a replayed step.
+thread_local char g_event_err[256];
+hipError_t record_event(hipEvent_t ev, gs_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t *deps = nullptr;
+  size_t ndeps = 0;
+  hipError_t e = hipStreamGetCaptureInfo_v2(s, &cs, nullptr, &graph, &deps, &ndeps);
+  if (e != hipSuccess) {
+    snprintf(g_event_err, sizeof(g_event_err), "%%s: hipStreamGetCaptureInfo_v2: %s", hipGetErrorString(e));
+    return e;
+  }
+  if (cs != hipStreamCaptureStatusActive) {
+    e = hipEventRecord(ev, s);
+    if (e != hipSuccess) snprintf(g_event_err, sizeof(g_event_err), "%%s: hipEventRecord: %s", hipGetErrorString(e));
+    return e;
+  }
+  // an event record node behind the capture's current frontier, which it
+  // then becomes (the documented way to add a node to a stream capture)
+  hipGraphNode_t node = nullptr;
+  e = hipGraphAddEventRecordNode(&node, graph, deps, ndeps, ev);
+  if (e == hipSuccess) e = hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+  if (e != hipSuccess) snprintf(g_event_err, sizeof(g_event_err), "%%s: event record node: %s", hipGetErrorString(e));
+  return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -127,7 +158,15 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   size_t need = 0;
   if (!fb_ok(a->fb, n, W, H, tiles, cells, &need))
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: frame workspace missing or below gs_frame_workspace_bytes", what);
-  if (!a->host_counters_dev || !a->host_counters_host)
+  // device_counts: no host read-back -- the T-dependent launches are sized by
+  // the tile workspace's capacity and read T (counters[5]) themselves
+  const bool dev = a->device_counts != 0;
+  if (dev && (a->fb.capacity <= 0 || a->resume))
+    return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: device_counts needs a tile workspace (capacity > 0), no resume",
+                            what);
+  if (dev && a->fb.flag_groups > 0 && a->fb.flag_groups < cells)
+    return gs_internal_fail(GS_ERR_UNSUPPORTED, "%s: device_counts renders tiles of one backward batch only", what);
+  if (!dev && (!a->host_counters_dev || !a->host_counters_host))
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: the pinned counter buffer (device and host address) is required",
                             what);
   const FrameLayout F = frame_layout(n, W, H, tiles, cells);
@@ -154,6 +193,10 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   ba.workspace_bytes = gs_bin_workspace_bytes(n > 0 ? n : 1);
   ba.pair_offset = pair_offset;
   ba.records = records;
+  ba.key_base = a->key_base;
+  ba.key_bits = a->key_bits;
+  ba.step_flags = a->step_flags;
+  ba.frame_seq = a->frame_seq;
   if (!a->resume) {
     a->M = a->T = 0;
     a->depth_min_bits = 0xFFFFFFFFu;
@@ -178,7 +221,7 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
     // a frame whose keys fit one workgroup sorts them there in one launch
     // (the same stable order as the radix passes it replaces)
     if (n <= gs_internal_small_sort_max()) {
-      st = gs_internal_small_sort(keys, nullptr, keys + un, vals + un, n, a->key_bits, stream);
+      st = gs_internal_small_sort(keys, nullptr, keys + un, vals + un, n, a->key_bits, nullptr, stream);
       alt = 1;
     } else if (a->depth_sort_msd && a->key_bits >= 9 && a->key_bits <= 31)
       st = gs_depth_sort_msd(keys, vals, keys + un, vals + un, n, a->key_bits, fw + F.sort_ws,
@@ -206,8 +249,16 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   const int32_t bits = tiles > 1 ? 32 - __builtin_clz((uint32_t)(tiles - 1)) : 1;
   const int32_t bits0 = gs_internal_first_pass_bits(0, bits);
   uint32_t *tile_counts =
-      (GS_EMIT_TILE_HIST && a->fb.capacity > 0) ? reinterpret_cast<uint32_t *>(tw + T0.sort_ws) : nullptr;
-  if (!a->resume) {
+      (GS_EMIT_TILE_HIST && a->fb.capacity > 0 && !dev) ? reinterpret_cast<uint32_t *>(tw + T0.sort_ws) : nullptr;
+  if (dev) {
+    // the count (status and T_eff on the device), the emission into the
+    // capacity (skipped by the kernel when T exceeds it), and on: no wait
+    ba.host_counters = a->host_counters_dev;
+    ba.host_seq = a->host_seq;
+    if ((st = gs_bin_count(&ba, stream))) return st;
+    if ((st = gs_bin_emit(&ba, stream))) return st;
+    a->M = a->T = -1;  // (on the device: counters[0..1], and the pinned buffer's copy)
+  } else if (!a->resume) {
     // the counts, then -- with a capacity guess -- the emission, queued before
     // the host reads (M, T) back: its kernel time hides the read-back
     ba.host_counters = a->host_counters_dev;
@@ -220,11 +271,21 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
       return st;
     // the one host synchronisation of a frame: poll the sequence word the
     // count writes through the pinned buffer's device address (no event, no copy)
+    // After 10 s of polling the stream is synchronised and the word read once
+    // more (a healthy stream may hold more than 10 s of work ahead of the
+    // count); only a count that has still not arrived then is an error.
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1; hc[4] != a->host_seq; ++i) {
       if ((i & 1023u) == 0) {
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-          return gs_internal_fail(GS_ERR_LAUNCH, "%s: the frame's counters never reached the host (10 s)", what);
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(a->poll_timeout_ms > 0 ? 0 : 10) +
+                                                        std::chrono::milliseconds(a->poll_timeout_ms)) {
+          if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+            return gs_internal_fail(GS_ERR_LAUNCH, "%s: hipStreamSynchronize failed while waiting for the counters",
+                                    what);
+          if (hc[4] != a->host_seq)
+            return gs_internal_fail(GS_ERR_LAUNCH, "%s: the frame's counters never reached the host", what);
+          break;
+        }
         sched_yield();
       }
     }
@@ -248,16 +309,20 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
     if ((st = tile_counts ? gs_internal_bin_emit_hist(&ba, tile_counts, bits0, stream) : gs_bin_emit(&ba, stream)))
       return st;
   }
-  const int32_t T = a->T;
+  // the entries the launches are sized for: T, or the capacity with the
+  // kernels reading T_eff (counters[5]: T, 0 for a failed frame) themselves
+  const int32_t T = dev ? (int32_t)a->fb.capacity : a->T;
+  const uint32_t *t_dev = dev ? counters + 5 : nullptr;
   int32_t talt = 0;
   uint32_t *tk = reinterpret_cast<uint32_t *>(tw + T0.tk[0]), *tk1 = reinterpret_cast<uint32_t *>(tw + T0.tk[1]);
   uint32_t *tv = reinterpret_cast<uint32_t *>(tw + T0.tv[0]), *tv1 = reinterpret_cast<uint32_t *>(tw + T0.tv[1]);
+  // (the one-workgroup sort and the radix passes are both stable: one order)
   if (T <= gs_internal_small_sort_max() && !tile_counts) {
-    if ((st = gs_internal_small_sort(tk, tv, tk1, tv1, T, bits, stream))) return st;
+    if ((st = gs_internal_small_sort(tk, tv, tk1, tv1, T, bits, t_dev, stream))) return st;
     talt = 1;
   } else if ((st = gs_internal_radix_sort_pairs(tk, tv, tk1, tv1, T, 0, bits, 0, tw + T0.sort_ws,
                                                 gs_radix_sort_workspace_bytes((int32_t)a->fb.capacity), &talt,
-                                                GS_EMIT_TILE_HIST ? 1 : 0, stream))) {
+                                                GS_EMIT_TILE_HIST ? 1 : 0, t_dev, stream))) {
     return st;
   }
   a->tile_alt = talt;
@@ -269,6 +334,7 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   ra.ranges = ranges;
   ra.slot_live = (a->zero_slot_flags && a->fb.flag_groups > 0) ? reinterpret_cast<uint8_t *>(tw + T0.flags) : nullptr;
   ra.cells = a->fb.flag_groups;
+  ra.num_pairs_dev = t_dev;
   if ((st = gs_tile_ranges(&ra, stream))) return st;
   gs_blend_fwd_args fa;
   memset(&fa, 0, sizeof(fa));
@@ -306,7 +372,13 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
   float *grad_sums = reinterpret_cast<float *>(fw + F.grad_sums);
   a->grad_sums = grad_sums;
   gs_status st;
-  const bool pixel_grads = a->M > 0 && a->T > 0 && a->g_image;
+  const bool dev = a->device_counts != 0;
+  if (dev && (a->fb.capacity <= 0 || G < cells))
+    return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: device_counts needs the forward's capacity and one batch", what);
+  // (device-resident: T unknown here -- the blend backward is launched over
+  // every tile, reads the ranges T_eff made, and the gather the frame status)
+  const bool pixel_grads = (dev || (a->M > 0 && a->T > 0)) && a->g_image;
+  const int32_t T = dev ? (int32_t)a->fb.capacity : a->T;
   if (pixel_grads) {
     if (!a->pair_grads || G < 1) return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: pair_grads / flag_groups", what);
     if (!a->image || !a->alpha || !a->depth)
@@ -336,7 +408,7 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
     b.live_words = (int64_t)T0.live_words;
     b.pair_grads = a->pair_grads;
     b.slot_live = flags;
-    b.num_pairs = a->T;
+    b.num_pairs = T;
     gs_project_bwd_args ga;
     memset(&ga, 0, sizeof(ga));
     ga.g.n = n;
@@ -346,20 +418,21 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
     ga.pair_grads = a->pair_grads;
     ga.slot_live = flags;
     ga.grad_sums = grad_sums;
+    ga.frame_status = dev ? reinterpret_cast<const uint32_t *>(fw + F.counters) + 4 : nullptr;
     hipEvent_t ev0 = (hipEvent_t)a->blend_events[0], ev1 = (hipEvent_t)a->blend_events[1];
-    if (ev0 && hipEventRecord(ev0, (hipStream_t)stream) != hipSuccess)
-      return gs_internal_fail(GS_ERR_LAUNCH, "%s: hipEventRecord failed", what);
+    if (ev0 && record_event(ev0, stream) != hipSuccess)
+      return gs_internal_fail(GS_ERR_LAUNCH, g_event_err, what);
     const int32_t one = gs_partial_groups(L);
     if (G >= one || G >= cells) {
       // one batch: every cell (or the tile's combined partials)
       b.cell_begin = 0;
       b.cell_count = 0;
       ga.partial_groups = G;
-      if (!a->flags_zeroed && hipMemsetAsync(flags, 0, (size_t)a->T * (size_t)G, (hipStream_t)stream) != hipSuccess)
+      if (!a->flags_zeroed && hipMemsetAsync(flags, 0, (size_t)T * (size_t)G, (hipStream_t)stream) != hipSuccess)
         return gs_internal_fail(GS_ERR_LAUNCH, "%s: slot flag memset failed", what);
       if ((st = gs_blend_backward(&b, stream))) return st;
-      if (ev1 && hipEventRecord(ev1, (hipStream_t)stream) != hipSuccess)
-        return gs_internal_fail(GS_ERR_LAUNCH, "%s: hipEventRecord failed", what);
+      if (ev1 && record_event(ev1, stream) != hipSuccess)
+        return gs_internal_fail(GS_ERR_LAUNCH, g_event_err, what);
       if ((st = gs_gather_partials(&ga, 0, stream))) return st;
     } else {
       // cell batches of G (bounded memory), summed in batch order
@@ -368,13 +441,13 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
         b.cell_count = cells - c0 < G ? cells - c0 : G;
         ga.partial_groups = b.cell_count;
         if ((bi || !a->flags_zeroed) &&
-            hipMemsetAsync(flags, 0, (size_t)a->T * (size_t)G, (hipStream_t)stream) != hipSuccess)
+            hipMemsetAsync(flags, 0, (size_t)T * (size_t)G, (hipStream_t)stream) != hipSuccess)
           return gs_internal_fail(GS_ERR_LAUNCH, "%s: slot flag memset failed", what);
         if ((st = gs_blend_backward(&b, stream))) return st;
         if ((st = gs_gather_partials(&ga, bi ? 1 : 0, stream))) return st;
       }
-      if (ev1 && hipEventRecord(ev1, (hipStream_t)stream) != hipSuccess)  // (batches: gathers included)
-        return gs_internal_fail(GS_ERR_LAUNCH, "%s: hipEventRecord failed", what);
+      if (ev1 && record_event(ev1, stream) != hipSuccess)  // (batches: gathers included)
+        return gs_internal_fail(GS_ERR_LAUNCH, g_event_err, what);
     }
   }
   if (!a->project) return GS_OK;  // (the caller runs gs_project_backward itself, e.g. per row range)

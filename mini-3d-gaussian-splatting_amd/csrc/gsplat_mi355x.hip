@@ -66,6 +66,7 @@ gs_status check_launch(const char *what) {
 }
 
 inline unsigned div_up(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+__device__ __forceinline__ uint32_t div_up_dev(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + b - 1) / b); }
 
 // torch.clamp semantics (NaN propagates)
 __device__ __forceinline__ float clamp01(float v) { return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
@@ -482,8 +483,19 @@ __global__ __launch_bounds__(kBlock) void k_project_fwd(gs_project_args a) {
 // of 64 (order = wave, round, lane: stable).  No global atomics: per-block
 // digit counts -> per-digit row scan (+ row totals) -> the scatter derives
 // the digit bases from the 256 totals itself.
+// n_dev (a device-resident frame's tile sort, launched before T is known on
+// the host): the items are min(*n_dev, n); n -- the capacity -- sizes the
+// grid and nb stays the count table's row stride.  Blocks past the items
+// leave at once; the scans run over the live blocks' columns only.
+__device__ __forceinline__ int live_items(int n, const uint32_t *n_dev) {
+  return n_dev ? (int)min((uint32_t)n, *n_dev) : n;
+}
+
 __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restrict__ keys, int n, int shift,
-                                                       int nbits, uint32_t *counts, int nb) {
+                                                       int nbits, uint32_t *counts, int nb,
+                                                       const uint32_t *n_dev = nullptr) {
+  n = live_items(n, n_dev);
+  if ((long long)blockIdx.x * kSortChunk >= n) return;
   __shared__ uint32_t hist[kRadix];
   hist[threadIdx.x] = 0;
   __syncthreads();
@@ -514,10 +526,12 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t *__restric
 // 256 * per stretch (loads all in flight): one block scan per stretch (nb <=
 // 4096, 8.4M keys: one) instead of one per 256 entries.
 constexpr int kScanPer = 16;
-__global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, uint32_t *totals, int nb) {
+__global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *counts, uint32_t *totals, int nb,
+                                                       const uint32_t *n_dev = nullptr) {
   __shared__ uint32_t s_tmp[4];
   const int d = blockIdx.x;
-  uint32_t *row = counts + (size_t)d * nb;
+  uint32_t *row = counts + (size_t)d * nb;  // (row stride: the launch's nb)
+  if (n_dev) nb = min(nb, (int)div_up_dev(*n_dev, kSortChunk));
   const int per = min(kScanPer, (nb + kBlock - 1) / kBlock);
   uint32_t carry = 0, tot;
   for (int c = 0; c < nb; c += kBlock * per) {
@@ -546,7 +560,10 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t *__rest
                                                           uint32_t *__restrict__ keys_out,
                                                           uint32_t *__restrict__ vals_out, int n, int shift,
                                                           int nbits, const uint32_t *counts,
-                                                          const uint32_t *totals, int nb) {
+                                                          const uint32_t *totals, int nb,
+                                                          const uint32_t *n_dev = nullptr) {
+  n = live_items(n, n_dev);
+  if ((long long)blockIdx.x * kSortChunk >= n) return;
   __shared__ uint32_t wcnt[4][kRadix];
   __shared__ uint32_t s_lbase[kRadix];  // block-local start of each digit
   __shared__ uint32_t s_gbase[kRadix];  // global start of this block's run of each digit
@@ -654,7 +671,9 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_bucket_sort(uint32_t *__res
                                                                const uint32_t *__restrict__ totals, int lowbits,
                                                                uint32_t *overflow, uint32_t whole_n = 0u,
                                                                uint32_t *__restrict__ keys_out = nullptr,
-                                                               uint32_t *__restrict__ vals_out = nullptr) {
+                                                               uint32_t *__restrict__ vals_out = nullptr,
+                                                               const uint32_t *whole_n_dev = nullptr) {
+  if (kWhole && whole_n_dev) whole_n = min(whole_n, *whole_n_dev);  // (a device-resident frame's T)
   __shared__ uint32_t s_k[kMsdCap], s_v[kMsdCap];
   __shared__ uint32_t wcnt[kMsdWaves][kRadix];
   __shared__ uint32_t s_lbase[kRadix];
@@ -904,8 +923,18 @@ __global__ __launch_bounds__(kBlock) void k_bin_partials(gs_bin_args a, uint32_t
 
 // exclusive scan of the touch partials (single block); counters[0] = M, [1] = T,
 // [2] / [3] = min / max visible depth bits (the projection's per-block values)
-__global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials, int nb, uint32_t *counters,
-                                                               uint32_t *host_counters, uint32_t host_seq) {
+// The depth-key window held (rasterizer.window_holds): every visible bits(Z)
+// - key_base below the window's limit -- 2^key_bits - 1, and 255 <<
+// (key_bits - 8) from 9 bits on (gs_depth_sort_msd's sentinel bucket).
+__device__ __forceinline__ bool window_held(uint32_t key_base, int key_bits, uint32_t zmin, uint32_t zmax) {
+  if (key_bits <= 0 || key_bits >= 32 || zmin > zmax) return true;
+  const uint64_t full = (1ull << key_bits) - 1ull;
+  const uint64_t lim = key_bits >= 9 ? min(full, 255ull << (key_bits - 8)) : full;
+  return zmin >= key_base && (uint64_t)(zmax - key_base) < lim;
+}
+
+__global__ __launch_bounds__(kBlock) void k_bin_scan_partials(gs_bin_args a, uint32_t *partials, int nb) {
+  uint32_t *const counters = a.counters, *const host_counters = a.host_counters;
   __shared__ uint32_t s_tmp3[3][kBlock / kWave];
   __shared__ uint32_t s_mm[2][kBlock / kWave];
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
@@ -958,17 +987,42 @@ __global__ __launch_bounds__(kBlock) void k_bin_scan_partials(uint32_t *partials
       mn = min(mn, s_mm[0][w]);
       mx = max(mx, s_mm[1][w]);
     }
+    // what a device-resident frame cannot do on the device (GS_FRAME_*): its
+    // later stages see T_eff = 0 entries (empty lists, memory-safe)
+    uint32_t status = 0u;
+    if ((long long)carry > a.capacity) status |= GS_FRAME_NEED_CAPACITY;
+    if (!window_held(a.key_base, a.key_bits, mn, mx)) status |= GS_FRAME_WINDOW_MISS;
+    if (vis == 0u) status |= GS_FRAME_EMPTY;
     counters[0] = vis;
     counters[1] = carry;
     counters[2] = mn;
     counters[3] = mx;
-    if (host_counters) {  // (M, T, depth range) straight to the host's pinned buffer
+    counters[4] = status;
+    counters[5] = status ? 0u : carry;
+    uint32_t seq = a.host_seq;
+    if (a.frame_seq) {  // (one block, one thread: a plain increment)
+      seq = *a.frame_seq + 1u;
+      *a.frame_seq = seq;
+    }
+    // the sticky step flags: the first frame that sets them is recorded for
+    // the host (its replays from there on updated nothing)
+    uint32_t sticky = status;
+    bool first_fail = status != 0u;
+    if (a.step_flags) {
+      const uint32_t old = atomicOr(a.step_flags, status);
+      sticky = old | status;
+      first_fail = old == 0u && status != 0u;
+    }
+    if (host_counters) {  // (M, T, depth range, status) straight to the host's pinned buffer
       host_counters[0] = vis;
       host_counters[1] = carry;
       host_counters[2] = mn;
       host_counters[3] = mx;
+      host_counters[5] = status;
+      host_counters[6] = sticky;
+      if (first_fail) host_counters[7] = seq;
       __threadfence_system();  // the counters reach the host before the sequence word
-      host_counters[4] = host_seq;
+      host_counters[4] = seq;
       __threadfence_system();
     }
   }
@@ -1151,7 +1205,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
 // 16-B flag store.  Same writes as k_tile_ranges.
 __global__ __launch_bounds__(kBlock) void k_tile_ranges4(gs_range_args a) {
   const long long p0 = 4 * ((long long)blockIdx.x * kBlock + threadIdx.x);
-  const long long T = a.num_pairs;
+  const long long T = live_items(a.num_pairs, a.num_pairs_dev);
   if (p0 > T) return;
   const int lane = threadIdx.x & 63;
   uint4 k = make_uint4(0u, 0u, 0u, 0u);
@@ -1191,6 +1245,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_ranges4(gs_range_args a) {
 
 __global__ __launch_bounds__(kBlock) void k_tile_ranges(gs_range_args a) {
   const long long p = (long long)blockIdx.x * kBlock + threadIdx.x;
+  a.num_pairs = live_items(a.num_pairs, a.num_pairs_dev);
   if (p > a.num_pairs) return;
   if (a.slot_live && p < a.num_pairs) {  // slot p's flags for the backward (coalesced)
     if (a.cells == 4)
@@ -1925,7 +1980,9 @@ __device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint3
   unpack_rect(a.rects, gi, tx0, tx1, ty0, ty1);
   uint32_t off32 = a.pair_offset[gi];
   asm volatile("" : "+v"(off32));
-  const uint32_t cnt = (valid && visb) ? rect_touches(tx0, tx1, ty0, ty1) : 0u;
+  // (a device-resident frame that failed has no partials to read: zero sums)
+  const bool frame_ok = !a.frame_status || *a.frame_status == 0u;
+  const uint32_t cnt = (valid && visb && frame_ok) ? rect_touches(tx0, tx1, ty0, ty1) : 0u;
   // lane q sums partial groups q, q + QL, ... of a slot's ng (one pass when ng <= QL)
   for (uint32_t qc = (uint32_t)q; cnt > (uint32_t)h && qc < ng; qc += QL) {
     const size_t off = off32;
@@ -2255,10 +2312,20 @@ __global__ __launch_bounds__(kBlock) void k_adam(gs_adam_args a, int4 firsts0, i
   for (int k = 1; k < GS_ADAM_MAX_TENSORS; ++k) ti += (int)blockIdx.x >= starts[k] ? 1 : 0;
   const gs_adam_tensor &t = a.t[ti];
   if (!t.grad) return;
+  // a replayed step whose frame failed on the device updates nothing (the
+  // caller redoes it); a replayed step's per-step scalars come from its row
+  if (a.skip_flag && *a.skip_flag) return;
+  float lr = t.lr, bc1 = t.bias_correction1, bc2s = t.bias_correction2_sqrt;
+  if (a.hyper) {
+    const float *h = a.hyper + ((size_t)*a.hyper_row * GS_ADAM_MAX_TENSORS + ti) * 3;
+    lr = h[0];
+    bc1 = h[1];
+    bc2s = h[2];
+  }
   float *const pout = t.param_out ? t.param_out : t.param;  // (in place unless an output is given)
   const int64_t base = (int64_t)(blockIdx.x - starts[ti]) * kAdamChunk;
   const float b1 = a.beta1, b2 = a.beta2, om1 = 1.f - b1, om2 = 1.f - b2;
-  const float step = t.lr / t.bias_correction1, bc2s = t.bias_correction2_sqrt;
+  const float step = lr / bc1;
   const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
                      reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq) |
                      reinterpret_cast<uintptr_t>(pout)) & 15) == 0;
@@ -2393,7 +2460,7 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
                               void *workspace, size_t workspace_bytes, int32_t *result_in_alt,
                               gs_stream_t stream) {
   return gs_internal_radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, begin_bit, end_bit, vals_are_iota,
-                                      workspace, workspace_bytes, result_in_alt, 0, stream);
+                                      workspace, workspace_bytes, result_in_alt, 0, nullptr, stream);
 }
 
 }  // extern "C"
@@ -2401,7 +2468,7 @@ gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt
 gs_status gs_internal_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
                                        int32_t n, int32_t begin_bit, int32_t end_bit, int32_t vals_are_iota,
                                        void *workspace, size_t workspace_bytes, int32_t *result_in_alt,
-                                       int32_t first_counts_ready, gs_stream_t stream) {
+                                       int32_t first_counts_ready, const uint32_t *n_dev, gs_stream_t stream) {
   if (!result_in_alt) return fail(GS_ERR_INVALID_ARG, "%s: null result_in_alt", "gs_radix_sort_pairs");
   if (begin_bit < 0 || end_bit > 32 || begin_bit >= end_bit || n < 0)
     return fail(GS_ERR_INVALID_ARG, "%s: bad bit range / n", "gs_radix_sort_pairs");
@@ -2424,12 +2491,14 @@ gs_status gs_internal_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t 
   int shift = begin_bit;
   for (int p = 0; p < passes; ++p) {
     const int nbits = (end_bit - shift) / (passes - p);
-    if (p > 0 || !first_counts_ready) k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, nb);
-    k_radix_scan<<<1 << nbits, kBlock, 0, s>>>(counts, totals, nb);
+    if (p > 0 || !first_counts_ready) k_radix_hist<<<nb, kBlock, 0, s>>>(kin, n, shift, nbits, counts, nb, n_dev);
+    k_radix_scan<<<1 << nbits, kBlock, 0, s>>>(counts, totals, nb, n_dev);
     if (p == 0 && vals_are_iota)
-      k_radix_scatter<true><<<nb, kBlock, 0, s>>>(kin, nullptr, kout, vout, n, shift, nbits, counts, totals, nb);
+      k_radix_scatter<true><<<nb, kBlock, 0, s>>>(kin, nullptr, kout, vout, n, shift, nbits, counts, totals, nb,
+                                                   n_dev);
     else
-      k_radix_scatter<false><<<nb, kBlock, 0, s>>>(kin, vin, kout, vout, n, shift, nbits, counts, totals, nb);
+      k_radix_scatter<false><<<nb, kBlock, 0, s>>>(kin, vin, kout, vout, n, shift, nbits, counts, totals, nb,
+                                                    n_dev);
     gs_status st = check_launch("gs_radix_sort_pairs");
     if (st) return st;
     shift += nbits;
@@ -2445,13 +2514,13 @@ gs_status gs_internal_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t 
 int32_t gs_internal_small_sort_max(void) { return kMsdCap; }
 
 gs_status gs_internal_small_sort(const uint32_t *keys, const uint32_t *vals, uint32_t *keys_out, uint32_t *vals_out,
-                                 int32_t n, int32_t bits, gs_stream_t stream) {
+                                 int32_t n, int32_t bits, const uint32_t *n_dev, gs_stream_t stream) {
   if (n < 0 || n > kMsdCap || bits < 1 || bits > 32 || (n > 0 && (!keys || !keys_out || !vals_out)))
     return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_internal_small_sort");
   if (n == 0) return GS_OK;
   k_msd_bucket_sort<true><<<1, kMsdThreads, 0, (hipStream_t)stream>>>(
       const_cast<uint32_t *>(keys), const_cast<uint32_t *>(vals), nullptr, bits, nullptr, (uint32_t)n, keys_out,
-      vals_out);
+      vals_out, n_dev);
   return check_launch("gs_internal_small_sort");
 }
 
@@ -2469,7 +2538,7 @@ gs_status gs_internal_bin_count_hist(const gs_bin_args *a, uint32_t *tile_counts
   const uint32_t zero = tile_counts ? (uint32_t)((1u << bits) * div_up(a->capacity > 0 ? a->capacity : 0, kSortChunk))
                                     : 0u;
   k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials, nb, TileHist{tile_counts, zero, 0});
-  k_bin_scan_partials<<<1, kBlock, 0, s>>>(partials, nb, a->counters, a->host_counters, a->host_seq);
+  k_bin_scan_partials<<<1, kBlock, 0, s>>>(*a, partials, nb);
   return check_launch("gs_bin_count");
 }
 
@@ -2523,7 +2592,7 @@ gs_status gs_bin_count(const gs_bin_args *a, gs_stream_t stream) {
   const int nb = (int)div_up(a->n, kBinChunk);
   uint32_t *partials = (uint32_t *)a->workspace;
   k_bin_partials<<<nb, kBlock, 0, s>>>(*a, partials, nb, TileHist{nullptr, 0u, 0});
-  k_bin_scan_partials<<<1, kBlock, 0, s>>>(partials, nb, a->counters, a->host_counters, a->host_seq);
+  k_bin_scan_partials<<<1, kBlock, 0, s>>>(*a, partials, nb);
   return check_launch("gs_bin_count");
 }
 
@@ -2701,7 +2770,7 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
 }
 
 gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream) {
-  if (!a || a->num_tensors < 0 || a->num_tensors > GS_ADAM_MAX_TENSORS)
+  if (!a || a->num_tensors < 0 || a->num_tensors > GS_ADAM_MAX_TENSORS || (a->hyper && !a->hyper_row))
     return fail(GS_ERR_INVALID_ARG, "%s: bad args", "gs_adam_step");
   int starts[GS_ADAM_MAX_TENSORS] = {0};
   long long nblk = 0;

@@ -1,0 +1,365 @@
+"""A training step replayed as one HIP graph, with no host synchronisation.
+
+The eager step (GaussianRenderer.render -> autograd backward -> FusedAdam)
+costs the host a read-back per frame: gs_render_forward polls the pinned
+counters for T before it can size the tile sort, the ranges and the blend
+(rasterizer._forward_frame), and every kernel is launched from Python through
+autograd.  GraphedStep removes both for a step whose camera, cotangents and
+Gaussian count stay fixed (the bench's step):
+
+  * the frame is device-resident (gs_render_fwd_args.device_counts): the
+    count writes (M, T, status) where the later kernels read them; the tile
+    sort, ranges and blends are launched for the tile workspace's capacity
+    and read T themselves; a frame whose T exceeds the capacity, whose depths
+    leave the depth-key window or that draws nothing is flagged (GS_FRAME_*)
+    and drawn with empty lists (memory-safe);
+  * render forward + backward + the FusedAdam update are captured once as a
+    HIP graph (_native.HipGraph) and replayed with one hipGraphLaunch;
+  * the Adam launch reads a sticky device flag the count sets and updates
+    nothing behind a failed frame (the GradScaler found-inf pattern); its
+    per-step lr and bias corrections come from a device table row picked by
+    the frame counter the count increments (a replay's arguments are fixed);
+  * the host reads the pinned counters one step behind (the GPU always has
+    the next replay queued): on a flag it synchronises, rewinds the skipped
+    steps' Adam step counts, redoes them eagerly (the eager path regrows the
+    tile workspace or re-renders with 32-bit depth keys), and captures again
+    with the new capacity and depth window.
+
+The replayed kernels are the eager path's kernels on the same inputs, so a
+replayed step equals the eager step bit for bit (tests/test_graph_step_gpu.py,
+with a forced capacity overflow and a forced window miss redone in between).
+Scope: this package's GaussianModel (raw scaling / rotation / opacity logit),
+DC colour (sh_degree 0), the default 16-px tile, one view per step.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import rasterizer as RZ
+from .renderer import camera_params
+
+HYPER_ROWS = 4096  # replays between two refills of the Adam hyper-parameter table (one sync each)
+
+
+class GraphedStep:
+    """step(): one render forward + backward of (camera, model) with fixed
+    cotangents on (image, alpha, depth), then optimizer.step() when an
+    optimizer is given -- replayed as a HIP graph after a first eager step.
+
+    eager_step: the same step through the public API (zero_grad, render,
+    backward, optimizer.step); it runs the first step, and redoes a replayed
+    step whose frame failed on the device.  Run the caller's own work on
+    `self.stream` (torch.cuda.stream(gstep.stream)) to keep everything on one
+    queue; otherwise each step joins the current stream both ways.
+
+    capacity / window: test knobs -- the tile workspace's capacity and the
+    depth-key window (key_base, key_bits) of the next capture (default: the
+    eager path's guesses, rasterizer._T_SEEN and rasterizer._window_for)."""
+
+    def __init__(self, renderer, camera, model, settings, cotangents: Sequence[torch.Tensor],
+                 optimizer=None, eager_step: Optional[Callable[[], None]] = None):
+        if not getattr(model, "_gs_fused_covariance", False):
+            raise ValueError("GraphedStep renders this package's GaussianModel (raw scaling / rotation)")
+        self.renderer, self.camera, self.model, self.settings, self.optimizer = (renderer, camera, model, settings,
+                                                                                 optimizer)
+        self.cam = camera_params(camera, settings, renderer.radius_min, renderer.radius_max, renderer.tile_size)
+        if self.cam.tile_size != N.GS_DEFAULT_TILE:
+            raise ValueError("GraphedStep renders the default 16-px tile")
+        sh = settings.sh_degree if settings.sh_degree is not None else int(getattr(model, "active_sh_degree", 0))
+        if sh:
+            raise ValueError("GraphedStep renders DC colour (sh_degree 0)")
+        self.dev = model._xyz.device
+        self.n = int(model._xyz.shape[0])
+        self.H, self.W = self.cam.image_height, self.cam.image_width
+        g_image, g_alpha, g_depth = (t.detach().to(self.dev, torch.float32).contiguous() for t in cotangents)
+        self.cot = (g_image.view(3, self.H, self.W), g_alpha.view(1, self.H, self.W), g_depth.view(1, self.H, self.W))
+        self.eager_step = eager_step or self._default_eager_step
+        self.stream = torch.cuda.Stream(device=self.dev)
+        self.sh = int(self.stream.cuda_stream)
+        self.graph: Optional[N.HipGraph] = None
+        self.disabled = False            # a frame that draws nothing (GS_FRAME_EMPTY): eager from then on
+        self.replays = 0                 # replays since the last capture / table refill (= frame_seq)
+        self.capacity: Optional[int] = None
+        self.window = "auto"
+        self.redone = []                 # (status bits, steps redone) per recovery
+        self.timing = False              # per-replay blend-backward event pairs (bench's live roofline)
+        self.event_pairs = []
+        self._raw_events = []
+        self._seen_lr = None
+        self._alloc_static()
+
+    # ------------------------------------------------------------------ setup
+    def _alloc_static(self):
+        lib, dev, n, f32 = N.load(), self.dev, self.n, torch.float32
+        H, W = self.H, self.W
+        self.lib = lib
+        self.means2d = torch.empty((n, 2), dtype=f32, device=dev)
+        self.conics = torch.empty((n, 2, 2), dtype=f32, device=dev)
+        self.radii = torch.empty((n,), dtype=f32, device=dev)
+        self.vis = torch.empty((n,), dtype=torch.bool, device=dev)
+        self.image = torch.empty((3, H, W), dtype=f32, device=dev)
+        self.alpha = torch.empty((1, H, W), dtype=f32, device=dev)
+        self.depth = torch.empty((1, H, W), dtype=f32, device=dev)
+        fws = int(lib.gs_frame_workspace_bytes(n, W, H, self.cam.tile_size))
+        self.frame_ws = torch.empty((fws,), dtype=torch.uint8, device=dev)
+        self.grads = {"xyz": torch.empty((n, 3), dtype=f32, device=dev),
+                      "scaling": torch.empty((n, 3), dtype=f32, device=dev),
+                      "rotation": torch.empty((n, 4), dtype=f32, device=dev),
+                      "color": torch.empty((n, 3), dtype=f32, device=dev),
+                      "opacity": torch.empty((n,), dtype=f32, device=dev)}
+        m = self.model
+        self.leaf_grad = [(m._xyz, self.grads["xyz"]), (m._scaling, self.grads["scaling"]),
+                          (m._rotation, self.grads["rotation"]),
+                          (m._features_dc, self.grads["color"].view(m._features_dc.shape)),
+                          (m._opacity, self.grads["opacity"].view(m._opacity.shape))]
+        # device words: [0] sticky step flags (Adam's skip flag), [1] frame counter (Adam's table row)
+        self.words = torch.zeros((64,), dtype=torch.int32, device=dev)
+        self.hyper = torch.zeros(((HYPER_ROWS + 1) * N.GS_ADAM_MAX_TENSORS * 3,), dtype=f32, device=dev)
+        self.hc = torch.zeros((8,), dtype=torch.int32, pin_memory=True)
+        self.hc_np = self.hc.numpy()
+        self.hc_dev = N.host_device_pointer(self.hc)
+        if self.hc_dev is None:
+            raise RuntimeError("GraphedStep needs pinned host memory the device can address")
+        self.tile_ws = self.pair_grads = None
+        self.ev = (N.RawEvent(), N.RawEvent())
+
+    def _adam_plan(self):
+        """(param, grad buffer) of every optimizer parameter the render
+        writes a gradient for, grouped as FusedAdam launches them (one
+        (betas, eps) group of <= GS_ADAM_MAX_TENSORS tensors)."""
+        by_leaf = {id(p): g for p, g in self.leaf_grad}
+        plan, key = [], None
+        for group in self.optimizer.param_groups:
+            for p in group["params"]:
+                if id(p) not in by_leaf:
+                    continue
+                k = (float(group["betas"][0]), float(group["betas"][1]), float(group["eps"]))
+                if key is not None and k != key:
+                    raise ValueError("GraphedStep: every rendered parameter needs the same betas / eps")
+                key = k
+                plan.append((p, by_leaf[id(p)], group))
+        if len(plan) > N.GS_ADAM_MAX_TENSORS:
+            raise ValueError("GraphedStep: more than GS_ADAM_MAX_TENSORS parameters")
+        return plan, key
+
+    def _fill_hyper(self):
+        """Rows 1..HYPER_ROWS of the Adam table: replay r applies step
+        state["step"] + r of each tensor, with FusedAdam.step's expressions
+        (Python doubles rounded to fp32, as its ctypes fields round them)."""
+        t = np.zeros(((HYPER_ROWS + 1), N.GS_ADAM_MAX_TENSORS, 3), dtype=np.float32)
+        b1, b2, _ = self.adam_key
+        lrs = []
+        for k, (p, _, group) in enumerate(self.plan):
+            base, lr = int(self.optimizer.state[p]["step"]), float(group["lr"])
+            lrs.append(lr)
+            for r in range(1, HYPER_ROWS + 1):
+                s = base + r
+                t[r, k] = (lr, 1.0 - b1 ** s, (1.0 - b2 ** s) ** 0.5)
+        self._seen_lr = tuple(lrs)
+        self.hyper.copy_(torch.from_numpy(t.reshape(-1)))
+
+    def _reset_counters(self):
+        """Frame counter and sticky flags to 0 (stream-ordered before the next
+        replay), the Adam table from the optimizer's current step counts."""
+        self.words.zero_()
+        self.hc.zero_()
+        self.replays = 0
+        if self.optimizer is not None:
+            self._fill_hyper()
+
+    def _capture(self):
+        """Buffers for this capacity and window, the argument structs, and the graph."""
+        lib, cam, dev = self.lib, self.cam, self.dev
+        tiles, cells, groups = cam.tiles_x * cam.tiles_y, cam.cells, cam.groups
+        seen = RZ._T_SEEN.get(dev, 0)
+        cap = self.capacity if self.capacity is not None else max(seen + seen // 4 + 4096, 4096)
+        if self.tile_ws is None or self._cap != cap:
+            tws = int(lib.gs_tile_workspace_bytes(cap, tiles, cells, groups))
+            self.tile_ws = torch.empty((tws,), dtype=torch.uint8, device=dev)
+            self.pair_grads = torch.empty((cap * groups, N.GS_PARTIAL_STRIDE), dtype=torch.float32, device=dev)
+            self._cap, self._tws = cap, tws
+        window = RZ._window_for(dev) if self.window == "auto" else self.window
+        m = self.model
+        fa = N.GsRenderFwdArgs()
+        fa.cam = cam.to_struct()
+        fa.g = RZ._build_gaussians_struct(self.n, m._xyz, None, m._scaling, m._rotation, m._features_dc,
+                                          m._opacity, opacity_is_logit=True)
+        fa.means2d, fa.conics, fa.radii, fa.vis = (self.means2d.data_ptr(), self.conics.data_ptr(),
+                                                   self.radii.data_ptr(), self.vis.data_ptr())
+        fa.image, fa.alpha, fa.depth = self.image.data_ptr(), self.alpha.data_ptr(), self.depth.data_ptr()
+        fb = fa.fb
+        fb.frame_ws, fb.frame_ws_bytes = self.frame_ws.data_ptr(), self.frame_ws.numel()
+        fb.tile_ws, fb.tile_ws_bytes, fb.capacity = self.tile_ws.data_ptr(), self._tws, cap
+        fb.live_cells, fb.flag_groups = cells, groups
+        fa.key_base, fa.key_bits = window if window is not None else (0, 32)
+        backoff = RZ._MSD_BACKOFF.get(dev, 0)
+        fa.depth_sort_msd = 1 if (RZ._DEPTH_MSD and window is not None and 9 <= fa.key_bits <= 31
+                                  and not backoff) else 0
+        fa.zero_slot_flags = 1
+        fa.host_counters_dev, fa.host_counters_host = self.hc_dev, self.hc.data_ptr()
+        fa.device_counts = 1
+        wp = self.words.data_ptr()
+        fa.step_flags, fa.frame_seq = wp, wp + 4
+        ba = N.GsRenderBwdArgs()
+        ba.cam, ba.fb, ba.g = fa.cam, fa.fb, fa.g
+        ba.M = ba.T = -1
+        ba.means2d, ba.conics, ba.vis = fa.means2d, fa.conics, fa.vis
+        ba.image, ba.alpha, ba.depth = fa.image, fa.alpha, fa.depth
+        ba.g_image, ba.g_alpha, ba.g_depth = (t.data_ptr() for t in self.cot)
+        ba.pair_grads = self.pair_grads.data_ptr()
+        ba.flags_zeroed, ba.project, ba.device_counts = 1, 1, 1
+        gr = self.grads
+        ba.d_xyz, ba.d_scaling, ba.d_rotation = gr["xyz"].data_ptr(), gr["scaling"].data_ptr(), gr["rotation"].data_ptr()
+        ba.d_color_logits, ba.d_opacity = gr["color"].data_ptr(), gr["opacity"].data_ptr()
+        ba.blend_events[0], ba.blend_events[1] = self.ev[0].handle, self.ev[1].handle
+        self.fa, self.ba, self.window_used = fa, ba, window
+        self.aa = None
+        if self.optimizer is not None:
+            self.plan, self.adam_key = self._adam_plan()
+            aa = N.GsAdamArgs()
+            aa.num_tensors = len(self.plan)
+            aa.beta1, aa.beta2, aa.eps = self.adam_key
+            for k, (p, g, _) in enumerate(self.plan):
+                st = self.optimizer.state[p]
+                out = self.optimizer.param_out.get(p)
+                aa.t[k] = N.GsAdamTensor(p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                                         g.data_ptr(), p.numel(), 0.0, 1.0, 1.0,
+                                         out.data_ptr() if out is not None else None)
+            aa.skip_flag, aa.hyper, aa.hyper_row = wp, self.hyper.data_ptr(), wp + 4
+            self.aa = aa
+        self._reset_counters()
+        if self.graph is not None:
+            self.graph.close()
+        torch.cuda.synchronize(dev)
+        self.graph = N.HipGraph(self.sh, self._enqueue)
+
+    def _enqueue(self):
+        lib, s = self.lib, self.sh
+        N.check(lib.gs_render_forward(C.byref(self.fa), s), "gs_render_forward (device-resident)")
+        self.ba.tile_alt = self.fa.tile_alt
+        N.check(lib.gs_render_backward(C.byref(self.ba), s), "gs_render_backward (device-resident)")
+        if self.aa is not None:
+            N.check(lib.gs_adam_step(C.byref(self.aa), s), "gs_adam_step (replayed)")
+
+    def _default_eager_step(self):
+        opt = self.optimizer
+        if opt is not None:
+            opt.zero_grad(set_to_none=True)
+        out = self.renderer.render(self.camera, self.model, self.settings)
+        torch.autograd.backward([out["image"], out["alpha"], out["depth"]], list(self.cot))
+        if opt is not None:
+            opt.step()
+
+    # ------------------------------------------------------------------- step
+    def _run_eager(self, k: int):
+        with torch.cuda.stream(self.stream):
+            for _ in range(k):
+                self.eager_step()
+
+    def step(self) -> None:
+        if self.disabled:
+            self._run_eager(1)
+            return
+        if self.graph is None:
+            self._run_eager(1)  # the first step: eager (Adam state, T and the depth range seen)
+            self._capture()
+            return
+        if self.optimizer is not None:
+            lrs = tuple(float(g["lr"]) for _, _, g in self.plan)
+            if self.replays >= HYPER_ROWS or lrs != self._seen_lr:
+                self.finish()  # (every launched replay checked; then a fresh table from here)
+                self._reset_counters()
+            for p, _, _ in self.plan:
+                self.optimizer.state[p]["step"] += 1
+        cur = N.stream_ptr(self.dev)
+        if cur != self.sh:
+            self.stream.wait_stream(torch.cuda.current_stream(self.dev))
+        if self.timing:
+            e0, e1 = self._event_pair()
+            self.graph.set_event(self.ev[0].handle, e0.handle)
+            self.graph.set_event(self.ev[1].handle, e1.handle)
+            self.event_pairs.append((e0, e1))
+        self.graph.launch()
+        self.replays += 1
+        if cur != self.sh:
+            torch.cuda.current_stream(self.dev).wait_stream(self.stream)
+        self._check(self.replays - 1)
+
+    def _event_pair(self):
+        i = 2 * len(self.event_pairs)
+        while len(self._raw_events) < i + 2:
+            self._raw_events.append(N.RawEvent())
+        return self._raw_events[i], self._raw_events[i + 1]
+
+    def blend_backward_ms(self):
+        """The blend backward's duration in each timed replay (after finish())."""
+        return [e0.elapsed_ms(e1) for e0, e1 in self.event_pairs]
+
+    def _wait_seq(self, upto: int, timeout_s: float = 10.0) -> None:
+        """Until the count of replay `upto` has written the pinned counters."""
+        if upto <= 0:
+            return
+        hv = self.hc_np
+        deadline = time.perf_counter() + timeout_s
+        i = 0
+        while int(hv[4]) - upto < 0:
+            i += 1
+            if (i & 255) == 0:
+                if time.perf_counter() > deadline:
+                    torch.cuda.synchronize(self.dev)  # (a long queue, not a lost count: look once more)
+                    if int(hv[4]) - upto < 0:
+                        raise RuntimeError("GraphedStep: a replay's counters never reached the host")
+                    break
+                time.sleep(0)
+
+    def _check(self, upto: int) -> None:
+        self._wait_seq(upto)
+        if int(self.hc_np[6]) != 0:
+            self._recover()
+
+    def finish(self) -> None:
+        """Synchronise and check every launched replay (redoing failed ones)."""
+        torch.cuda.synchronize(self.dev)
+        if self.graph is not None and not self.disabled:
+            self._check(self.replays)
+
+    def _recover(self) -> None:
+        """A replayed frame failed on the device: every replay from the first
+        failed one on updated nothing (the sticky flag).  Rewind their Adam
+        step counts, redo them eagerly, capture again for the new capacity /
+        depth window (or stay eager after an empty frame)."""
+        torch.cuda.synchronize(self.dev)
+        hv = self.hc_np
+        flags, first = int(hv[6]), int(hv[7])
+        skipped = self.replays - first + 1
+        if not (1 <= skipped <= self.replays):
+            raise RuntimeError(f"GraphedStep: inconsistent failure record (first {first}, replays {self.replays})")
+        if self.optimizer is not None:
+            for p, _, _ in self.plan:
+                self.optimizer.state[p]["step"] -= skipped
+        self.redone.append((flags, skipped))
+        self._run_eager(skipped)
+        if flags & N.GS_FRAME_EMPTY:
+            self.disabled = True  # (the same camera and model draw nothing again)
+            return
+        if flags & N.GS_FRAME_NEED_CAPACITY:
+            self.capacity = None  # (the eager frames' T is the next guess)
+        if flags & N.GS_FRAME_WINDOW_MISS:
+            self.window = "auto"
+        self._capture()
+
+    def assign_grads(self) -> None:
+        """Point the parameters' .grad at the last replay's gradients."""
+        for p, g in self.leaf_grad:
+            p.grad = g
+
+    def close(self) -> None:
+        if self.graph is not None:
+            self.graph.close()
+            self.graph = None

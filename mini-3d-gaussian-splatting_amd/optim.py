@@ -10,8 +10,10 @@ Parameters without .grad are skipped, as torch does.
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 
 import torch
+from torch.optim import optimizer as _OPT
 
 from . import _native as N
 
@@ -61,6 +63,8 @@ class FusedAdam(torch.optim.Optimizer):
     def _launch(batches, lo=None, hi=None):
         """One gs_adam_step per (betas, eps) batch of <= 8 tensors, over rows
         [lo, hi) of each (dim 0; all rows when lo is None)."""
+        if not batches:
+            return
         lib = N.load()
         stream = N.stream_ptr()
         for (b1, b2, eps), ds in batches.items():
@@ -95,14 +99,43 @@ class FusedAdam(torch.optim.Optimizer):
                             p.grad.requires_grad_(False)
                         p.grad.zero_()
 
+    def _hooks_registered(self) -> bool:
+        return bool(self._optimizer_step_pre_hooks or self._optimizer_step_post_hooks
+                    or _OPT._global_optimizer_pre_hooks or _OPT._global_optimizer_post_hooks)
+
+    def _hooked(self, fn, args, kwargs):
+        """fn(*args, **kwargs) between the registered step pre / post hooks,
+        in torch.optim.Optimizer's order and with its argument rewriting
+        (torch's profile_hook_step wrapper, which `step.hooked` skips)."""
+        for hook in itertools.chain(_OPT._global_optimizer_pre_hooks.values(),
+                                    self._optimizer_step_pre_hooks.values()):
+            res = hook(self, args, kwargs)
+            if res is not None:
+                if isinstance(res, tuple) and len(res) == 2:
+                    args, kwargs = res
+                else:
+                    raise RuntimeError(f"{hook} must return None or a tuple of (new_args, new_kwargs), "
+                                       f"but got {res}.")
+        out = fn(*args, **kwargs)
+        for hook in itertools.chain(self._optimizer_step_post_hooks.values(),
+                                    _OPT._global_optimizer_post_hooks.values()):
+            hook(self, args, kwargs)
+        return out
+
     @torch.no_grad()
     def step(self, closure=None):
         """One Adam step over every parameter with a gradient.  The launch
         descriptors are kept between steps and only the per-step fields
         (gradient address, lr, bias corrections) rewritten while the
-        parameters, moments and outputs stay where they were.  (torch's
-        Optimizer step hooks and profiler annotation are not run: step is
-        marked hooked, see below.)"""
+        parameters, moments and outputs stay where they were.  torch's
+        profiler annotation is not run (step is marked hooked, see below);
+        registered step pre / post hooks (per optimizer or global) are, when
+        there are any (checking costs two dict tests)."""
+        if self._hooks_registered():
+            return self._hooked(self._step, (closure,), {})
+        return self._step(closure)
+
+    def _step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -130,6 +163,8 @@ class FusedAdam(torch.optim.Optimizer):
                 plan.append((p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                              out.data_ptr() if out is not None else 0, p.numel(), float(b1), float(b2), float(eps)))
                 per_step.append((g, float(lr), 1.0 - b1 ** t, (1.0 - b2 ** t) ** 0.5))
+        if not plan:
+            return loss  # (no parameter has a gradient: nothing to launch)
         key = tuple(plan)
         cached = getattr(self, "_plan_cache", None)
         if cached is None or cached[0] != key:
@@ -169,6 +204,11 @@ class FusedAdam(torch.optim.Optimizer):
         when given, runs before range k is queued -- the data-parallel
         reducer makes the stream wait for range k's all-reduce there, so
         range k's update overlaps the reductions of the ranges after it."""
+        if self._hooks_registered():
+            return self._hooked(self._step_ranges, (ranges, before), {})
+        return self._step_ranges(ranges, before)
+
+    def _step_ranges(self, ranges, before=None):
         batches = self._begin()
         for k, (lo, hi) in enumerate(ranges):
             if before is not None:

@@ -274,7 +274,7 @@ def _check_inputs(xyz: torch.Tensor):
 class _Frame:
     """Intermediate device buffers of one forward, kept for the backward."""
     __slots__ = ("records", "rects", "vis", "pair_offset", "order", "ranges", "sorted_gauss", "pix_flags",
-                 "cell_neval", "live_bits", "big", "M", "T", "slot_live", "groups")
+                 "cell_neval", "live_bits", "big", "M", "T", "slot_live", "groups", "consumed")
 
 
 _T_SEEN: dict = {}  # device -> tile entries T of its last frame (capacity guess)
@@ -651,6 +651,7 @@ def forward_pipeline(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, o
 
     fr = _Frame()
     fr.slot_live = None
+    fr.consumed = False  # (a backward ran: the slot flags hold its last batch's, not the forward's zeros)
     fr.groups = cam.groups
     fr.records, fr.rects, fr.vis, fr.order = records, rects, vis, None
     if n > 0:
@@ -832,6 +833,11 @@ def backward_pipeline(cam: CameraParams, fr: _Frame, xyz, cov3d, scaling, rotati
         slot_live = fr.slot_live  # (zeroed by the forward's gs_tile_ranges)
         if slot_live is None:
             slot_live = torch.zeros((fr.T * G,), dtype=torch.uint8, device=dev)
+        elif fr.consumed:
+            # a second backward of the frame (retain_graph): the flags hold the
+            # last batch's, in that batch's layout
+            slot_live.zero_()
+        fr.consumed = True
         ba = N.GsBlendBwdArgs(cs, cam.tiles_x, cam.tiles_y, N.ptr(fr.ranges), N.ptr(fr.sorted_gauss),
                               N.ptr(fr.records), N.ptr(image), N.ptr(alpha), N.ptr(depth),
                               N.ptr(fr.pix_flags), N.ptr(fr.cell_neval), N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth), N.ptr(fr.live_bits),
@@ -935,6 +941,7 @@ def _backward_frame(cam: CameraParams, fr: _FastFrame, xyz, cov3d, scaling, rota
         ba.g_image, ba.g_alpha, ba.g_depth = N.ptr(g_image), N.ptr(g_alpha), N.ptr(g_depth)
         ba.pair_grads = pair_grads.data_ptr()
         ba.flags_zeroed = 1 if fr.slot_live_zeroed else 0
+        fr.slot_live_zeroed = False  # (a second backward of the frame clears its flags first: ADVICE r05)
     gm = None if g_means2d is None else g_means2d.contiguous()
     gc = None if g_conics is None else g_conics.contiguous()
     ba.g_means2d, ba.g_conics = N.ptr(gm), N.ptr(gc)

@@ -33,20 +33,26 @@ offsets with ncclAvg on the collective stream behind an event -- on
 rank-dependent integer-valued data, checks the mean on every rank, and checks
 ncclCommCount / ncclCommUserRank against the process group.
 
-Limitation: ncclCommInitRank (step 3) blocks until every rank has joined the
-communicator's bootstrap.  The agreement after step 2 means every rank enters
-it, but a rank that fails inside it before joining (e.g. a device error on
-that rank alone) leaves the others blocked in the call, where no agreement
-can reach them; only the self-check (step 4) is bounded in time.  A
-non-blocking init (ncclCommInitRankConfig with blocking = 0, then polling
-ncclCommGetAsyncError) would bound it too, but would also make every later
-call on the communicator asynchronous (ncclInProgress), a mode this module's
-call sequence was never run in on more than one GPU; it is not used.
+Bounded in time: ncclCommInitRank (step 3) blocks until
+every rank has joined the communicator's bootstrap, so a rank that fails
+inside it before joining (a device error on that rank alone, a transport that
+never connects) would leave the others blocked in the call, where no
+agreement can reach them.  The call therefore runs on a helper thread (with
+the rank's device made current there); the rank waits for it at most
+INIT_TIMEOUT_S and then joins the agreement either way.  A rank whose init
+has not returned by then reports failure, every rank falls back to
+torch.distributed at that step, and the stuck thread is abandoned (if its
+call ever returns, the thread aborts the communicator it got).  The
+self-check collective (step 4) is bounded by SELF_CHECK_TIMEOUT_S.  (A
+non-blocking init, ncclCommInitRankConfig with blocking = 0, would make every
+later call on the communicator asynchronous -- ncclInProgress -- a mode this
+module's call sequence was never run in on more than one GPU.)
 """
 from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
 import time
 from typing import List, Sequence, Tuple
 
@@ -62,6 +68,9 @@ HIP_ERROR_NOT_READY = 600
 # communicator also sets up its connections); past it the check fails on this
 # rank, and with it the native path on every rank
 SELF_CHECK_TIMEOUT_S = float(os.environ.get("GS_RCCL_CHECK_TIMEOUT", "60"))
+# seconds ncclCommInitRank may take on its helper thread before this rank
+# reports the init failed (every rank then falls back together)
+INIT_TIMEOUT_S = float(os.environ.get("GS_RCCL_INIT_TIMEOUT", "60"))
 
 
 class _UniqueId(C.Structure):
@@ -186,8 +195,9 @@ class RcclComm:
             self._abort()
             raise RcclError(err0 or "ncclGetUniqueId failed on rank 0")
         C.memmove(C.addressof(uid), got[:128], 128)
-        # 3. the communicator; 4. the self-check collective
-        step("ncclCommInitRank", lambda: self._init_comm(uid))
+        # 3. the communicator (bounded in time: a helper thread); 4. the
+        # self-check collective (bounded too)
+        step("ncclCommInitRank", lambda: self._init_comm_bounded(uid))
         step("self-check", self._self_check)
 
     # -- construction steps (overridable: tests drive the protocol with fakes) --
@@ -197,6 +207,41 @@ class RcclComm:
 
     def _get_unique_id(self, uid: "_UniqueId") -> None:
         _check_nccl(self._rccl, self._rccl.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
+
+    def _init_comm_bounded(self, uid: "_UniqueId") -> None:
+        """_init_comm on a helper thread, waited for at most INIT_TIMEOUT_S.
+        Past it this rank reports failure (RcclError) and abandons the thread:
+        the thread, should its call ever return, aborts the communicator
+        itself (under the lock, so exactly one side owns it)."""
+        lock, st, done = threading.Lock(), {"finished": False, "abandoned": False, "err": None}, threading.Event()
+
+        def run():
+            try:
+                if self.device is not None and self.device.type == "cuda":
+                    torch.cuda.set_device(self.device)  # (HIP's current device is per thread)
+                self._init_comm(uid)
+            except BaseException as e:  # noqa: BLE001 -- reported by the waiting thread
+                st["err"] = e
+            finally:
+                with lock:
+                    st["finished"] = True
+                    abandoned = st["abandoned"]
+                if abandoned and self._comm and getattr(self, "_rccl", None) is not None:
+                    self._rccl.ncclCommAbort(self._comm)
+                    self._comm = C.c_void_p()
+                done.set()
+
+        th = threading.Thread(target=run, name=f"rccl-init-rank{self.rank}", daemon=True)
+        th.start()
+        done.wait(INIT_TIMEOUT_S)
+        with lock:
+            if not st["finished"]:
+                st["abandoned"] = True
+        if st["abandoned"]:
+            self._init_abandoned = True  # (_abort leaves the communicator to the thread)
+            raise RcclError(f"ncclCommInitRank did not return within {INIT_TIMEOUT_S:g} s on rank {self.rank}")
+        if st["err"] is not None:
+            raise st["err"]
 
     def _init_comm(self, uid: "_UniqueId") -> None:
         rccl = self._rccl
@@ -234,7 +279,7 @@ class RcclComm:
     def _abort(self) -> None:
         """Drop a half-built communicator without waiting for other ranks."""
         rccl, hip = getattr(self, "_rccl", None), getattr(self, "_hip", None)
-        if self._comm and rccl is not None:
+        if self._comm and rccl is not None and not getattr(self, "_init_abandoned", False):
             try:
                 rccl.ncclCommAbort(self._comm)
             finally:

@@ -1,5 +1,6 @@
 """Data-parallel grad all-reduce over gloo, world_size 2, CPU."""
 import os
+import time
 import socket
 
 import pytest
@@ -284,6 +285,9 @@ def _worker_native_decision(rank, world, port, q, fail):
                 assert uid.internal.startswith(b"fake-id")  # rank 0's id reached every rank
                 if fail == "init" and self.rank == 1:
                     raise RcclError("ncclCommInitRank: invalid usage (5)")
+                if fail == "init_hang" and self.rank == 1:
+                    import threading
+                    threading.Event().wait()  # (never returns: a rank stuck in the bootstrap)
                 self.nranks = self.world
 
             def _self_check(self):
@@ -293,6 +297,8 @@ def _worker_native_decision(rank, world, port, q, fail):
                 self.self_check = 0.0
 
         factory = Fake
+        rccl.INIT_TIMEOUT_S = 3.0  # (the hang case: both ranks must be back well within the test's limit)
+        t0 = time.monotonic()
         if fail == "import" and rank == 1:
             # this rank cannot import the native module: the real _native_comm path
             sys.modules[pkg.__name__ + ".rccl"] = None
@@ -303,12 +309,12 @@ def _worker_native_decision(rank, world, port, q, fail):
         t = torch.tensor([float(rank + 1)])
         dist.all_reduce(t)
         pkg.distributed.close_native_comms()
-        q.put((rank, comm is not None, st, calls, float(t)))
+        q.put((rank, comm is not None, st, calls, float(t), time.monotonic() - t0))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fail", [None, "load", "uid", "init", "check", "import"])
+@pytest.mark.parametrize("fail", [None, "load", "uid", "init", "init_hang", "check", "import"])
 def test_native_comm_decided_by_all_ranks_gloo(fail):
     """Round-3 review item 3 / advisor: the native-RCCL choice is collective.
     Whichever construction step fails on one rank (library load, rank 0's
@@ -323,10 +329,10 @@ def test_native_comm_decided_by_all_ranks_gloo(fail):
     procs = [ctx.Process(target=_worker_native_decision, args=(r, 2, port, q, fail)) for r in range(2)]
     for p in procs:
         p.start()
-    res = {}
+    res, took = {}, {}
     for _ in range(2):
-        r, native, st, calls, tsum = q.get(timeout=120)
-        res[r] = (native, st, calls, tsum)
+        r, native, st, calls, tsum, dt = q.get(timeout=120)
+        res[r], took[r] = (native, st, calls, tsum), dt
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -341,7 +347,7 @@ def test_native_comm_decided_by_all_ranks_gloo(fail):
             assert st["rccl_nranks"] is None and st["fallback_reason"]
     # both ranks stop after the same step (rank 0 alone makes the unique id)
     done = {None: ["load", "init", "check"], "load": ["load"], "uid": ["load"], "init": ["load", "init"],
-            "check": ["load", "init", "check"]}
+            "init_hang": ["load", "init"], "check": ["load", "init", "check"]}
     if fail in done:
         for r in (0, 1):
             assert [c for c in res[r][2] if c != "uid"] == done[fail]
@@ -354,6 +360,12 @@ def test_native_comm_decided_by_all_ranks_gloo(fail):
         assert "ncclGetUniqueId" in res[0][1]["fallback_reason"] and "rank 0" in res[1][1]["fallback_reason"]
     if fail == "import":
         assert "import rccl" in res[1][1]["fallback_reason"] and "another rank" in res[0][1]["fallback_reason"]
+    if fail == "init_hang":
+        # a rank stuck in ncclCommInitRank reports failure
+        # after INIT_TIMEOUT_S (3 s here); both ranks fall back, neither hangs
+        assert "did not return within 3 s on rank 1" in res[1][1]["fallback_reason"]
+        assert "another rank" in res[0][1]["fallback_reason"]
+        assert max(took.values()) < 30.0
 
 
 def test_self_check_wait_is_bounded():

@@ -229,3 +229,27 @@ def test_host_scalars_and_struct_caches(pkg):
     assert g2.opacity_is_logit == 0 and g.opacity_is_logit == 1
     xyz2 = torch.zeros(5, 3)
     assert RZ._gaussians_struct(5, xyz2, None, sc, rot, col, op, True).xyz == xyz2.data_ptr()
+
+
+def test_fused_adam_runs_step_hooks(pkg):
+    """torch.optim.Optimizer's step pre / post hooks (per optimizer
+    and global) run around FusedAdam.step and step_ranges, in torch's order;
+    a pre hook may rewrite the arguments.  (No gradients: nothing launches.)"""
+    import torch
+    from torch.optim.optimizer import register_optimizer_step_post_hook
+    p = torch.nn.Parameter(torch.zeros(3))
+    opt = pkg.optim.FusedAdam([p])
+    calls = []
+    h1 = opt.register_step_pre_hook(lambda o, a, k: calls.append(("pre", a)))
+    h2 = opt.register_step_post_hook(lambda o, a, k: calls.append(("post", a)))
+    h3 = register_optimizer_step_post_hook(lambda o, a, k: calls.append(("global_post", a)))
+    try:
+        assert opt.step() is None
+        opt.step_ranges([(0, 3)])
+    finally:
+        h1.remove(), h2.remove(), h3.remove()
+    assert [c[0] for c in calls] == ["pre", "post", "global_post"] * 2
+    assert calls[0][1] == (None,) and calls[3][1] == ([(0, 3)], None)
+    calls.clear()
+    opt.step()
+    assert calls == []
