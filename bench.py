@@ -92,6 +92,10 @@ def parse():
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one HIP graph over a device-resident frame (graph_step.GraphedStep; "
                          "auto: at world size 1 with the optimizer) or run it eagerly through autograd")
+    ap.add_argument("--fused-adam", choices=("auto", "on", "off"), default="auto",
+                    help="replayed steps: the optimizer in the backward (gs_project_backward_adam: the "
+                         "projection backward applies the Adam update, no gradient tensor materialised; auto: on "
+                         "with --graph at world size 1) or the separate gs_adam_step launch")
     a = ap.parse_args()
     n0, w0, h0 = CONFIGS[a.config]
     a.gaussians = n0 if a.gaussians is None else a.gaussians
@@ -243,7 +247,8 @@ def main():
     use_graph = a.graph == "on" or (a.graph == "auto" and reducer is None and opt is not None)
     gstep = None
     if use_graph:
-        gstep = pkg.GraphedStep(renderer, cam, model, settings, cot, opt, eager_step=eager_step)
+        fused = a.fused_adam == "on" or (a.fused_adam == "auto" and world == 1)
+        gstep = pkg.GraphedStep(renderer, cam, model, settings, cot, opt, eager_step=eager_step, fused_adam=fused)
         torch.cuda.set_stream(gstep.stream)  # (every step, eager or replayed, on the graph's queue)
         step = gstep.step
     else:
@@ -280,6 +285,9 @@ def main():
                       "steps_redone_in_timed_region": sum(k for _, k in gstep.redone) - redone0,
                       "redone": gstep.redone, "disabled": gstep.disabled,
                       "capacity": gstep._cap, "depth_window_bits": (gstep.window_used or (0, 32))[1],
+                      "optimizer": ("FusedAdam in the projection backward (gs_project_backward_adam): the same "
+                                    "update, no gradient tensor materialised, no separate Adam launch"
+                                    if gstep.fused_adam else "FusedAdam, one gs_adam_step launch"),
                       "note": "render fwd + bwd + FusedAdam captured once (hipStreamBeginCapture) over a "
                               "device-resident frame and replayed with hipGraphLaunch; no host read-back"}
     else:

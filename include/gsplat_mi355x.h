@@ -444,6 +444,19 @@ typedef struct gs_adam_args {
 } gs_adam_args;
 gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream);
 
+/* Optimizer in the backward (opt-in; one rank, no gradient hooks): the
+ * projection backward of the training configuration (raw scaling / rotation,
+ * opacity logit, DC colour, blend sums in grad_sums or pair_grads, no
+ * viewspace / conic cotangents) applies the Adam update of gs_adam_step --
+ * the same fp32 operations -- to each parameter where its gradient is formed,
+ * instead of writing d_* (not read; no gradient reaches HBM).  adam->t[0..4]
+ * are xyz, colour logits, opacity logit, scaling, rotation: param = the arrays
+ * of a->g (dense rows), their moments, param_out (NULL: in place); grad is
+ * ignored.  skip_flag / hyper / hyper_row as in gs_adam_args.  Saves the
+ * gradients' write and read and the parameters' second read (~168 B per
+ * Gaussian) and a launch.  GS_ERR_UNSUPPORTED outside that configuration. */
+gs_status gs_project_backward_adam(const gs_project_bwd_args *a, const gs_adam_args *adam, gs_stream_t stream);
+
 /* ---- Photometric loss ---------------------------------
  * total = (1 - lambda) * L1 + lambda * D-SSIM, the objective of GaussianLoss
  * (src/core/loss.py:41-63): L1 = mean |pred - target| (:56); D-SSIM =
@@ -600,6 +613,8 @@ typedef struct gs_render_bwd_args {
                                       after the blend backward launch(es): its time alone (profiling) */
   int32_t device_counts;           /* the forward was device-resident: M, T are not read; pair_grads holds
                                       capacity * flag_groups partials; the gather reads the frame status */
+  const gs_adam_args *fused_adam;  /* with project = 1: gs_project_backward_adam with these tensors (no
+                                      d_* written), or NULL: the plain projection backward */
 } gs_render_bwd_args;
 gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream);
 /* Byte offsets of the buffers inside the two workspaces (for diagnostics and

@@ -137,7 +137,7 @@ class GsRenderBwdArgs(C.Structure):
         ("alpha", _vp), ("depth", _vp), ("g_image", _vp), ("g_alpha", _vp), ("g_depth", _vp), ("g_means2d", _vp), ("g_conics", _vp), ("pair_grads", _vp),
         ("flags_zeroed", C.c_int32), ("project", C.c_int32), ("d_xyz", _vp), ("d_cov3d", _vp),
         ("d_scaling", _vp), ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
-        ("grad_sums", _vp), ("blend_events", _vp * 2), ("device_counts", C.c_int32),
+        ("grad_sums", _vp), ("blend_events", _vp * 2), ("device_counts", C.c_int32), ("fused_adam", _vp),
     ]
 
 
@@ -196,7 +196,7 @@ EXPORTS = (
     "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_workspace_bytes", "gs_bin_count", "gs_bin_emit",
     "gs_tile_ranges", "gs_blend_live_words", "gs_tile_quads", "gs_partial_groups", "gs_blend_forward", "gs_blend_backward", "gs_project_backward",
     "gs_blend_backward_groups", "gs_blend_backward_lane_stats", "gs_gather_partials", "gs_frame_workspace_bytes", "gs_tile_workspace_bytes", "gs_render_forward",
-    "gs_render_backward", "gs_frame_offsets", "gs_tile_offsets", "gs_adam_step", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
+    "gs_render_backward", "gs_frame_offsets", "gs_tile_offsets", "gs_adam_step", "gs_project_backward_adam", "gs_loss_workspace_bytes", "gs_loss_forward", "gs_loss_backward",
     "gs_densify_workspace_bytes", "gs_densify_count", "gs_densify_emit",
 )
 
@@ -248,6 +248,7 @@ def _declare(lib):
     lib.gs_tile_offsets.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32, P(C.c_size_t)]
     lib.gs_tile_offsets.restype = None
     lib.gs_adam_step.argtypes = [P(GsAdamArgs), _vp]
+    lib.gs_project_backward_adam.argtypes = [P(GsProjectBwdArgs), P(GsAdamArgs), _vp]
     lib.gs_loss_workspace_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32]
     lib.gs_loss_workspace_bytes.restype = C.c_size_t
     lib.gs_loss_forward.argtypes = [P(GsLossArgs), _vp]
@@ -258,7 +259,7 @@ def _declare(lib):
     lib.gs_densify_emit.argtypes = [P(GsDensifyArgs), _vp]
     for f in ("gs_project_forward", "gs_radix_sort_pairs", "gs_depth_sort_msd", "gs_bin_count", "gs_bin_emit",
               "gs_tile_ranges", "gs_blend_forward", "gs_blend_backward", "gs_blend_backward_lane_stats",
-              "gs_project_backward", "gs_gather_partials", "gs_render_forward", "gs_render_backward", "gs_adam_step", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
+              "gs_project_backward", "gs_gather_partials", "gs_render_forward", "gs_render_backward", "gs_adam_step", "gs_project_backward_adam", "gs_loss_forward", "gs_loss_backward", "gs_densify_count", "gs_densify_emit"):
         getattr(lib, f).restype = C.c_int
 
 

@@ -470,6 +470,7 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
   pb.d_opacity = a->d_opacity;
   pb.d_sh_rest = a->d_sh_rest;
   pb.grad_sums = pixel_grads ? grad_sums : nullptr;  // (the sums are there: no gather here)
+  if (a->fused_adam) return gs_project_backward_adam(&pb, a->fused_adam, stream);
   return gs_project_backward(&pb, stream);
 }
 

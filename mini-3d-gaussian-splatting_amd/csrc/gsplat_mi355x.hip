@@ -2060,8 +2060,69 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, 
 
 // Gaussian g's chain rule from its summed blend gradients: sums(acc) fills
 // acc[10] (from k_gather_slots' [n, 10] sums, or the fused gather's LDS)
-template <bool kHot, typename Sums>
-__device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, int g, Sums sums) {
+// Where project_bwd_one's gradients go: out(tensor, element, gradient,
+// parameter value) -- the gradient arrays (GradsOut), or, with the optimizer
+// fused into the backward, an Adam update of the parameter (AdamOut).
+enum : int { kOutXyz = 0, kOutColor = 1, kOutOpacity = 2, kOutScaling = 3, kOutRotation = 4, kOutCov = 5 };
+struct GradsOut {
+  const gs_project_bwd_args &a;
+  __device__ __forceinline__ void operator()(int t, size_t i, float grad, float) const {
+    switch (t) {
+      case kOutXyz: a.d_xyz[i] = grad; break;
+      case kOutColor: a.d_color_logits[i] = grad; break;
+      case kOutOpacity: a.d_opacity[i] = grad; break;
+      case kOutScaling: a.d_scaling[i] = grad; break;
+      case kOutRotation: a.d_rotation[i] = grad; break;
+      default: a.d_cov3d[i] = grad; break;
+    }
+  }
+};
+
+// gs_project_backward_adam: FusedAdam's update (k_adam's arithmetic, the same
+// fp32 operations in the same order) applied where the gradient is formed;
+// the parameter value is the one the chain rule read.  Tensors in the
+// kOut* order; skip: a failed device-resident frame updates nothing.
+struct FusedAdamArgs {
+  float *param_out[5], *exp_avg[5], *exp_avg_sq[5];
+  float lr[5], bc1[5], bc2s[5];
+  float beta1, beta2, eps;
+  const uint32_t *skip_flag;
+  const float *hyper;        // [row][GS_ADAM_MAX_TENSORS][3] (gs_adam_args.hyper) or NULL
+  const uint32_t *hyper_row;
+  int hyper_slot[5];         // the tensor's slot in a hyper row
+};
+struct AdamOut {
+  const FusedAdamArgs &f;
+  float step[5], bc2s[5];
+  __device__ __forceinline__ explicit AdamOut(const FusedAdamArgs &fa) : f(fa) {
+    const uint32_t row = f.hyper ? *f.hyper_row : 0u;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      float lr = f.lr[t], bc1 = f.bc1[t], b2s = f.bc2s[t];
+      if (f.hyper) {
+        const float *h = f.hyper + ((size_t)row * GS_ADAM_MAX_TENSORS + f.hyper_slot[t]) * 3;
+        lr = h[0];
+        bc1 = h[1];
+        b2s = h[2];
+      }
+      step[t] = lr / bc1;
+      bc2s[t] = b2s;
+    }
+  }
+  __device__ __forceinline__ void operator()(int t, size_t i, float grad, float p) const {
+    if (t > kOutRotation) return;  // (no covariance input on the fused path)
+    const float om1 = 1.f - f.beta1, om2 = 1.f - f.beta2;
+    float m = f.exp_avg[t][i], v = f.exp_avg_sq[t][i];
+    m = m + om1 * (grad - m);
+    v = f.beta2 * v + om2 * (grad * grad);
+    f.param_out[t][i] = p - step[t] * (m / (sqrtf(v) / bc2s[t] + f.eps));
+    f.exp_avg[t][i] = m;
+    f.exp_avg_sq[t][i] = v;
+  }
+};
+
+template <bool kHot, typename Sums, typename Out>
+__device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, int g, Sums sums, const Out &out) {
   float scl_pre[3] = {0.f, 0.f, 0.f}, rot_pre[4] = {0.f, 0.f, 0.f, 0.f}, op_pre = 0.f;
   if constexpr (kHot) {
 #pragma unroll
@@ -2095,7 +2156,7 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
   for (int k = 0; k < 3; ++k) {
     const float c = 1.f / (1.f + expf(-cl[k]));
     dlg[k] = acc[6 + k] * c * (1.f - c);
-    a.d_color_logits[3 * (size_t)g + k] = dlg[k];
+    out(kOutColor, 3 * (size_t)g + k, dlg[k], cl[k]);
   }
   // SH: d rest_k = Y_k dlogit; the view direction's gradient reaches xyz
   // through dir = v / |v| (added to d_xyz below)
@@ -2124,21 +2185,22 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
     const float o = 1.f / (1.f + expf(-(kHot ? op_pre : a.g.opacity[(int64_t)g * a.g.opacity_stride])));
     dop = (dop * (1.f - o)) * o;
   }
-  a.d_opacity[g] = dop;
+  out(kOutOpacity, (size_t)g, dop, op_pre);
   const bool any = dm0 != 0.f || dm1 != 0.f || G[0] != 0.f || G[1] != 0.f || G[2] != 0.f ||
                    G[3] != 0.f || acc[9] != 0.f;
   const bool raw = kHot || a.g.cov3d == nullptr;
   if (!any) {
+    const float xv[3] = {xw, yw, zw};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.d_xyz[3 * (size_t)g + k] = dxyz_sh[k];
+    for (int k = 0; k < 3; ++k) out(kOutXyz, 3 * (size_t)g + k, dxyz_sh[k], xv[k]);
     if (raw) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) a.d_scaling[3 * (size_t)g + k] = 0.f;
+      for (int k = 0; k < 3; ++k) out(kOutScaling, 3 * (size_t)g + k, 0.f, scl_pre[k]);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) a.d_rotation[4 * (size_t)g + k] = 0.f;
+      for (int k = 0; k < 4; ++k) out(kOutRotation, 4 * (size_t)g + k, 0.f, rot_pre[k]);
     } else {
 #pragma unroll
-      for (int k = 0; k < 9; ++k) a.d_cov3d[9 * (size_t)g + k] = 0.f;
+      for (int k = 0; k < 9; ++k) out(kOutCov, 9 * (size_t)g + k, 0.f, 0.f);
     }
     return;
   }
@@ -2203,9 +2265,12 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
   const double dZ = dm0 * (-fx * X * iz2) + dm1 * (fy * Y * iz2) + dJ[0] * (-fx * iz2) +
                     dJ[2] * (2.0 * fx * X * iz3) + dJ[4] * (fy * iz2) + dJ[5] * (-2.0 * fy * Y * iz3) +
                     (double)acc[9];
+  {
+    const float xv[3] = {xw, yw, zw};
 #pragma unroll
-  for (int j = 0; j < 3; ++j)
-    a.d_xyz[3 * (size_t)g + j] = (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ + (double)dxyz_sh[j]);
+    for (int j = 0; j < 3; ++j)
+      out(kOutXyz, 3 * (size_t)g + j, (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ + (double)dxyz_sh[j]), xv[j]);
+  }
   float J[6], dV[4];
 #pragma unroll
   for (int k = 0; k < 6; ++k) J[k] = (float)Jd[k];
@@ -2231,7 +2296,7 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
     for (int j = 0; j < 3; ++j) dS[i * 3 + j] = dot3(R[i], R[4 + i], R[8 + i], dCR[j], dCR[3 + j], dCR[6 + j]);
   if (!raw) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) a.d_cov3d[9 * (size_t)g + k] = dS[k];
+    for (int k = 0; k < 9; ++k) out(kOutCov, 9 * (size_t)g + k, dS[k], 0.f);
     return;
   }
   // raw path: Sigma = M M^T, M = R(q) diag(s), s = exp(scaling), q = normalize(rotation)
@@ -2257,7 +2322,7 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
       dR[i * 3 + j] = dot3(Ss[i * 3], Ss[i * 3 + 1], Ss[i * 3 + 2], Rq[j], Rq[3 + j], Rq[6 + j]) * (s3[j] * s3[j]);
 #pragma unroll
   for (int j = 0; j < 3; ++j)  // dL/ds_j s_j: (dR / s_j) . Rq column j, times s_j
-    a.d_scaling[3 * (size_t)g + j] = dot3(dR[j], dR[3 + j], dR[6 + j], Rq[j], Rq[3 + j], Rq[6 + j]);
+    out(kOutScaling, 3 * (size_t)g + j, dot3(dR[j], dR[3 + j], dR[6 + j], Rq[j], Rq[3 + j], Rq[6 + j]), sc[j]);
   const float dw = 2.f * ((-z * dR[1] + y * dR[2]) + (z * dR[3] - x * dR[5]) + (-y * dR[6] + x * dR[7]));
   const float dx = 2.f * ((y * dR[1] + z * dR[2]) + (y * dR[3] - 2.f * x * dR[4]) + (-w * dR[5] + z * dR[6]) +
                           (w * dR[7] - 2.f * x * dR[8]));
@@ -2266,23 +2331,26 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
   const float dz = 2.f * ((-2.f * z * dR[0] - w * dR[1]) + (x * dR[2] + w * dR[3]) + (-2.f * z * dR[4] + y * dR[5]) +
                           (x * dR[6] + y * dR[7]));
   const float dot = __builtin_fmaf(dw, w, __builtin_fmaf(dx, x, __builtin_fmaf(dy, y, dz * z)));
-  a.d_rotation[4 * (size_t)g + 0] = (dw - w * dot) * iq;
-  a.d_rotation[4 * (size_t)g + 1] = (dx - x * dot) * iq;
-  a.d_rotation[4 * (size_t)g + 2] = (dy - y * dot) * iq;
-  a.d_rotation[4 * (size_t)g + 3] = (dz - z * dot) * iq;
+  out(kOutRotation, 4 * (size_t)g + 0, (dw - w * dot) * iq, rq[0]);
+  out(kOutRotation, 4 * (size_t)g + 1, (dx - x * dot) * iq, rq[1]);
+  out(kOutRotation, 4 * (size_t)g + 2, (dy - y * dot) * iq, rq[2]);
+  out(kOutRotation, 4 * (size_t)g + 3, (dz - z * dot) * iq, rq[3]);
 }
 
 // kHot: partials present, no viewspace/conic cotangents, raw scale/rotation,
 // DC colour -- the training configuration.  Its loads are all issued up
 // front (a load under a runtime branch is waited for at the branch's join,
 // which serialised six round trips per thread in the generic instantiation).
-template <bool kHot>
-__global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
+// kAdam (gs_project_backward_adam, kHot only): the parameters' Adam update
+// fused in, no gradient arrays written.
+template <bool kHot, bool kAdam = false>
+__global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a, FusedAdamArgs fa = {}) {
   const int k = blockIdx.x * kBlock + threadIdx.x;
   if (k >= a.g.n) return;
+  if (kAdam && fa.skip_flag && *fa.skip_flag) return;  // (the replayed step's frame failed)
   // in depth order, consecutive threads own adjacent slot ranges
   const int g = (!kHot && a.order) ? (int)a.order[k] : k;
-  project_bwd_one<kHot>(a, g, [&](float acc[GS_PAIR_GRAD_FLOATS]) {
+  auto sums = [&](float acc[GS_PAIR_GRAD_FLOATS]) {
 #pragma unroll
     for (int k = 0; k < GS_PAIR_GRAD_FLOATS; ++k) acc[k] = 0.f;
     if (kHot || a.grad_sums) {  // g's partials summed (k_gather_slots)
@@ -2294,7 +2362,11 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a) {
         acc[2 * k + 1] = v.y;
       }
     }
-  });
+  };
+  if constexpr (kAdam)
+    project_bwd_one<kHot>(a, g, sums, AdamOut(fa));
+  else
+    project_bwd_one<kHot>(a, g, sums, GradsOut{a});
 }
 
 // tile coordinates are packed in 12 bits (record word 11): images up to 65536 px a side
@@ -2767,6 +2839,55 @@ gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream) 
   else
     k_project_bwd<false><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a);
   return check_launch("gs_project_backward");
+}
+
+gs_status gs_project_backward_adam(const gs_project_bwd_args *a, const gs_adam_args *adam, gs_stream_t stream) {
+  static const char *what = "gs_project_backward_adam";
+  if (!a || !adam) return fail(GS_ERR_INVALID_ARG, "%s: null args", what);
+  if (a->g.n <= 0) return GS_OK;
+  // the training configuration only (k_project_bwd<kHot>): raw scale /
+  // rotation, DC colour, blend sums, no viewspace / conic cotangents
+  if (a->g.cov3d || a->g.sh_degree != 0 || a->g_means2d || a->g_conics || a->order || !a->grad_sums ||
+      !a->g.scaling || !a->g.rotation || !a->g.opacity_is_logit)
+    return fail(GS_ERR_UNSUPPORTED, "%s: raw scaling / rotation, opacity logit, DC colour, blend sums, no "
+                "viewspace / conic cotangents", what);
+  if (!a->g.xyz || !a->g.color_logits || !a->means2d || !a->conics || !a->vis || !a->rects || !a->pair_offset ||
+      (a->pair_grads && (!a->slot_live || a->partial_groups < 1)) || adam->num_tensors != 5 ||
+      (adam->hyper && !adam->hyper_row) || !cam_ok(a->cam))
+    return fail(GS_ERR_INVALID_ARG, "%s: null buffer, or adam->num_tensors != 5", what);
+  // the tensors in the kOut* order, each the parameter the projection reads
+  const float *params[5] = {a->g.xyz, a->g.color_logits, a->g.opacity, a->g.scaling, a->g.rotation};
+  const int64_t rows[5] = {3, 3, 1, 3, 4};
+  FusedAdamArgs f;
+  memset(&f, 0, sizeof(f));
+  for (int t = 0; t < 5; ++t) {
+    const gs_adam_tensor &x = adam->t[t];
+    if (x.param != params[t] || !x.exp_avg || !x.exp_avg_sq || x.numel != rows[t] * a->g.n)
+      return fail(GS_ERR_INVALID_ARG, "%s: adam->t[0..4] must be xyz, colour logits, opacity, scaling, rotation "
+                  "(the projection's own parameter arrays, dense)", what);
+    f.param_out[t] = x.param_out ? x.param_out : x.param;
+    f.exp_avg[t] = x.exp_avg;
+    f.exp_avg_sq[t] = x.exp_avg_sq;
+    f.lr[t] = x.lr;
+    f.bc1[t] = x.bias_correction1;
+    f.bc2s[t] = x.bias_correction2_sqrt;
+    f.hyper_slot[t] = t;
+  }
+  if (a->g.xyz_stride != 3 || a->g.color_stride != 3 || a->g.opacity_stride != 1)
+    return fail(GS_ERR_INVALID_ARG, "%s: dense parameter rows", what);
+  f.beta1 = adam->beta1;
+  f.beta2 = adam->beta2;
+  f.eps = adam->eps;
+  f.skip_flag = adam->skip_flag;
+  f.hyper = adam->hyper;
+  f.hyper_row = adam->hyper_row;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->pair_grads) {
+    gs_status st = launch_gather(a, 0, s);
+    if (st) return st;
+  }
+  k_project_bwd<true, true><<<div_up(a->g.n, kBlock), kBlock, 0, s>>>(*a, f);
+  return check_launch(what);
 }
 
 gs_status gs_adam_step(const gs_adam_args *a, gs_stream_t stream) {

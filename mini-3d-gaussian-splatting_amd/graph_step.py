@@ -63,7 +63,7 @@ class GraphedStep:
     eager path's guesses, rasterizer._T_SEEN and rasterizer._window_for)."""
 
     def __init__(self, renderer, camera, model, settings, cotangents: Sequence[torch.Tensor],
-                 optimizer=None, eager_step: Optional[Callable[[], None]] = None):
+                 optimizer=None, eager_step: Optional[Callable[[], None]] = None, fused_adam: bool = False):
         if not getattr(model, "_gs_fused_covariance", False):
             raise ValueError("GraphedStep renders this package's GaussianModel (raw scaling / rotation)")
         self.renderer, self.camera, self.model, self.settings, self.optimizer = (renderer, camera, model, settings,
@@ -80,6 +80,17 @@ class GraphedStep:
         g_image, g_alpha, g_depth = (t.detach().to(self.dev, torch.float32).contiguous() for t in cotangents)
         self.cot = (g_image.view(3, self.H, self.W), g_alpha.view(1, self.H, self.W), g_depth.view(1, self.H, self.W))
         self.eager_step = eager_step or self._default_eager_step
+        # the optimizer in the backward (gs_project_backward_adam, VERDICT r05
+        # item 5): the projection backward applies the Adam update where each
+        # gradient is formed; no gradient tensor is written (assign_grads() is
+        # then unavailable).  Replayed steps only: the redo path is eager.
+        self.fused_adam = bool(fused_adam)
+        if self.fused_adam:
+            if optimizer is None:
+                raise ValueError("fused_adam needs the optimizer")
+            for p in (model._xyz, model._features_dc, model._opacity, model._scaling, model._rotation):
+                if getattr(p, "_backward_hooks", None) or getattr(p, "_post_accumulate_grad_hooks", None):
+                    raise ValueError("fused_adam: a parameter has gradient hooks (no gradient is materialised)")
         self.stream = torch.cuda.Stream(device=self.dev)
         self.sh = int(self.stream.cuda_stream)
         self.graph: Optional[N.HipGraph] = None
@@ -146,6 +157,14 @@ class GraphedStep:
                 plan.append((p, by_leaf[id(p)], group))
         if len(plan) > N.GS_ADAM_MAX_TENSORS:
             raise ValueError("GraphedStep: more than GS_ADAM_MAX_TENSORS parameters")
+        if self.fused_adam:
+            # gs_project_backward_adam's tensor order: xyz, colour logits,
+            # opacity logit, scaling, rotation -- every one in the optimizer
+            m = self.model
+            order = [id(t) for t in (m._xyz, m._features_dc, m._opacity, m._scaling, m._rotation)]
+            if sorted(order) != sorted(id(p) for p, _, _ in plan):
+                raise ValueError("fused_adam: the optimizer must hold the five rendered parameters")
+            plan.sort(key=lambda e: order.index(id(e[0])))
         return plan, key
 
     def _fill_hyper(self):
@@ -233,6 +252,8 @@ class GraphedStep:
                                          out.data_ptr() if out is not None else None)
             aa.skip_flag, aa.hyper, aa.hyper_row = wp, self.hyper.data_ptr(), wp + 4
             self.aa = aa
+            if self.fused_adam:
+                ba.fused_adam = C.addressof(aa)  # (the projection backward updates; no Adam launch)
         self._reset_counters()
         if self.graph is not None:
             self.graph.close()
@@ -244,7 +265,7 @@ class GraphedStep:
         N.check(lib.gs_render_forward(C.byref(self.fa), s), "gs_render_forward (device-resident)")
         self.ba.tile_alt = self.fa.tile_alt
         N.check(lib.gs_render_backward(C.byref(self.ba), s), "gs_render_backward (device-resident)")
-        if self.aa is not None:
+        if self.aa is not None and not self.fused_adam:
             N.check(lib.gs_adam_step(C.byref(self.aa), s), "gs_adam_step (replayed)")
 
     def _default_eager_step(self):
@@ -356,6 +377,8 @@ class GraphedStep:
 
     def assign_grads(self) -> None:
         """Point the parameters' .grad at the last replay's gradients."""
+        if self.fused_adam:
+            raise RuntimeError("fused_adam: the replayed steps write no gradients")
         for p, g in self.leaf_grad:
             p.grad = g
 

@@ -133,3 +133,24 @@ def test_graph_event_pairs_time_the_blend_backward(pkg, cuda):
     ms = gs.blend_backward_ms()
     assert len(ms) == 4 and all(0.0 < x < 50.0 for x in ms), ms
     gs.close()
+
+
+def test_fused_adam_in_the_projection_backward(pkg, cuda):
+    """the optimizer in the backward
+    (gs_project_backward_adam) -- replayed steps whose projection backward
+    applies the Adam update itself, no gradient written -- equal eager steps
+    (autograd + FusedAdam.step) bit for bit: parameters, moments, step counts,
+    with shadow outputs and in place; a failed frame is skipped there too."""
+    for shadow in (False, True):
+        ma, oa, cam, st, cot = _setup(pkg, cuda, seed=5, shadow=shadow)
+        _eager(pkg, ma, oa, cam, st, cot, 6)
+        mb, ob, cam_b, st_b, cot_b = _setup(pkg, cuda, seed=5, shadow=shadow)
+        gs = pkg.GraphedStep(pkg.GaussianRenderer(), cam_b, mb, st_b, cot_b, ob, fused_adam=True)
+        gs.capacity = 512  # (one failed replay pair, redone: the fused update skipped on the device)
+        with torch.cuda.stream(gs.stream):
+            for _ in range(6):
+                gs.step()
+        gs.finish()
+        assert len(gs.redone) == 1 and gs.redone[0][0] & pkg._native.GS_FRAME_NEED_CAPACITY
+        _assert_same_state(ma, oa, mb, ob)
+        gs.close()
