@@ -377,8 +377,9 @@ typedef struct gs_project_bwd_args {
   const uint8_t *vis;
   const uint32_t *rects;
   const uint32_t *pair_offset;
-  const uint32_t *order;       /* [n] permutation to walk the Gaussians in, or NULL: index order
-                                  (slots are numbered in index order, so NULL reads them coalesced) */
+  const uint32_t *order;       /* [n] permutation to walk the Gaussians in (the gather and the
+                                  projection backward), or NULL: index order (slots are numbered in
+                                  index order, so NULL reads them coalesced) */
   const float *pair_grads;     /* [T,G,GS_PARTIAL_STRIDE] (G = partial_groups), summed into grad_sums
                                   first; NULL: no blend gradient (T == 0), or -- with grad_sums --
                                   the sums are already there (gs_gather_partials, cell batches) */

@@ -1964,10 +1964,11 @@ constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
 #endif
 constexpr int kGatherNB = GS_GATHER_NB;
 template <int QL, int HL, int kNG>
-__device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint32_t ng, long long t, float2 acc[kF2]) {
+__device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint32_t ng, long long t, int g,
+                                             float2 acc[kF2]) {
   constexpr int LPG = QL * HL;
   static_assert(LPG == 2 || LPG == 4 || LPG == 8, "lanes per Gaussian");
-  const int g = (int)(t / LPG), h = (int)((t % LPG) / QL), q = (int)(t % QL);
+  const int h = (int)((t % LPG) / QL), q = (int)(t % QL);
 #pragma unroll
   for (int k = 0; k < kF2; ++k) acc[k] = make_float2(0.f, 0.f);
   // vis, rect and first slot in one round trip (the empty asm keeps the
@@ -2040,9 +2041,10 @@ template <int QL, int HL, int kNG = 0>  // kNG > 0: the partial groups per slot 
 __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng_rt, int accumulate) {
   constexpr int LPG = QL * HL;
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const int g = (int)(t / LPG);
+  int g = (int)(t / LPG);
+  if (a.order && g < a.g.n) g = (int)a.order[g];  // (a walk in another order: gs_project_bwd_args.order)
   float2 acc[kF2];
-  gather_slots<QL, HL, kNG>(a, kNG > 0 ? (uint32_t)kNG : ng_rt, t, acc);
+  gather_slots<QL, HL, kNG>(a, kNG > 0 ? (uint32_t)kNG : ng_rt, t, g, acc);
   if ((t % LPG) == 0 && g < a.g.n) {
     float2 *out = reinterpret_cast<float2 *>(a.grad_sums) + (size_t)g * kF2;
     if (accumulate) {
@@ -2060,28 +2062,31 @@ __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, 
 
 // Gaussian g's chain rule from its summed blend gradients: sums(acc) fills
 // acc[10] (from k_gather_slots' [n, 10] sums, or the fused gather's LDS)
-// Where project_bwd_one's gradients go: out(tensor, element, gradient,
-// parameter value) -- the gradient arrays (GradsOut), or, with the optimizer
-// fused into the backward, an Adam update of the parameter (AdamOut).
+// Where project_bwd_one's gradients go: out(tensor, g, k, gradient,
+// parameter value) for element k of Gaussian g's row -- the gradient arrays
+// (GradsOut), or, with the optimizer fused into the backward, a register
+// buffer whose Adam update flush() applies once the row is complete
+// (AdamOut).
 enum : int { kOutXyz = 0, kOutColor = 1, kOutOpacity = 2, kOutScaling = 3, kOutRotation = 4, kOutCov = 5 };
 struct GradsOut {
   const gs_project_bwd_args &a;
-  __device__ __forceinline__ void operator()(int t, size_t i, float grad, float) const {
+  __device__ __forceinline__ void operator()(int t, int g, int k, float grad, float) const {
     switch (t) {
-      case kOutXyz: a.d_xyz[i] = grad; break;
-      case kOutColor: a.d_color_logits[i] = grad; break;
-      case kOutOpacity: a.d_opacity[i] = grad; break;
-      case kOutScaling: a.d_scaling[i] = grad; break;
-      case kOutRotation: a.d_rotation[i] = grad; break;
-      default: a.d_cov3d[i] = grad; break;
+      case kOutXyz: a.d_xyz[3 * (size_t)g + k] = grad; break;
+      case kOutColor: a.d_color_logits[3 * (size_t)g + k] = grad; break;
+      case kOutOpacity: a.d_opacity[g] = grad; break;
+      case kOutScaling: a.d_scaling[3 * (size_t)g + k] = grad; break;
+      case kOutRotation: a.d_rotation[4 * (size_t)g + k] = grad; break;
+      default: a.d_cov3d[9 * (size_t)g + k] = grad; break;
     }
   }
 };
 
 // gs_project_backward_adam: FusedAdam's update (k_adam's arithmetic, the same
-// fp32 operations in the same order) applied where the gradient is formed;
-// the parameter value is the one the chain rule read.  Tensors in the
-// kOut* order; skip: a failed device-resident frame updates nothing.
+// fp32 operations in the same order) applied to the 14 parameters of a
+// Gaussian once its gradients are formed; the parameter value is the one the
+// chain rule read.  Tensors in the kOut* order; skip: a failed
+// device-resident frame updates nothing.
 struct FusedAdamArgs {
   float *param_out[5], *exp_avg[5], *exp_avg_sq[5];
   float lr[5], bc1[5], bc2s[5];
@@ -2091,11 +2096,28 @@ struct FusedAdamArgs {
   const uint32_t *hyper_row;
   int hyper_slot[5];         // the tensor's slot in a hyper row
 };
+constexpr int kAdamRow[5] = {3, 3, 1, 3, 4};   // floats per Gaussian, kOut* order
+constexpr int kAdamOff[6] = {0, 3, 6, 7, 10, 14};
 struct AdamOut {
-  const FusedAdamArgs &f;
-  float step[5], bc2s[5];
-  __device__ __forceinline__ explicit AdamOut(const FusedAdamArgs &fa) : f(fa) {
+  float gv[14], pv[14];  // the row's gradients and parameter values (registers after unrolling)
+  __device__ __forceinline__ void operator()(int t, int, int k, float grad, float p) {
+    if (t > kOutRotation) return;  // (no covariance input on the fused path)
+    gv[kAdamOff[t] + k] = grad;
+    pv[kAdamOff[t] + k] = p;
+  }
+  // every m and v of the row requested in one round trip, then the updates
+  __device__ __forceinline__ void flush(const FusedAdamArgs &f, int g) const {
     const uint32_t row = f.hyper ? *f.hyper_row : 0u;
+    float m[14], v[14];
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int k = 0; k < kAdamRow[t]; ++k) {
+        const size_t i = (size_t)kAdamRow[t] * g + k;
+        m[kAdamOff[t] + k] = f.exp_avg[t][i];
+        v[kAdamOff[t] + k] = f.exp_avg_sq[t][i];
+      }
+    const float om1 = 1.f - f.beta1, om2 = 1.f - f.beta2;
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
       float lr = f.lr[t], bc1 = f.bc1[t], b2s = f.bc2s[t];
@@ -2105,24 +2127,24 @@ struct AdamOut {
         bc1 = h[1];
         b2s = h[2];
       }
-      step[t] = lr / bc1;
-      bc2s[t] = b2s;
+      const float step = lr / bc1;
+#pragma unroll
+      for (int k = 0; k < kAdamRow[t]; ++k) {
+        const int j = kAdamOff[t] + k;
+        const size_t i = (size_t)kAdamRow[t] * g + k;
+        const float gr = gv[j];
+        const float mm = m[j] + om1 * (gr - m[j]);
+        const float vv = f.beta2 * v[j] + om2 * (gr * gr);
+        f.param_out[t][i] = pv[j] - step * (mm / (sqrtf(vv) / b2s + f.eps));
+        f.exp_avg[t][i] = mm;
+        f.exp_avg_sq[t][i] = vv;
+      }
     }
-  }
-  __device__ __forceinline__ void operator()(int t, size_t i, float grad, float p) const {
-    if (t > kOutRotation) return;  // (no covariance input on the fused path)
-    const float om1 = 1.f - f.beta1, om2 = 1.f - f.beta2;
-    float m = f.exp_avg[t][i], v = f.exp_avg_sq[t][i];
-    m = m + om1 * (grad - m);
-    v = f.beta2 * v + om2 * (grad * grad);
-    f.param_out[t][i] = p - step[t] * (m / (sqrtf(v) / bc2s[t] + f.eps));
-    f.exp_avg[t][i] = m;
-    f.exp_avg_sq[t][i] = v;
   }
 };
 
 template <bool kHot, typename Sums, typename Out>
-__device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, int g, Sums sums, const Out &out) {
+__device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, int g, Sums sums, Out &out) {
   float scl_pre[3] = {0.f, 0.f, 0.f}, rot_pre[4] = {0.f, 0.f, 0.f, 0.f}, op_pre = 0.f;
   if constexpr (kHot) {
 #pragma unroll
@@ -2156,7 +2178,7 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
   for (int k = 0; k < 3; ++k) {
     const float c = 1.f / (1.f + expf(-cl[k]));
     dlg[k] = acc[6 + k] * c * (1.f - c);
-    out(kOutColor, 3 * (size_t)g + k, dlg[k], cl[k]);
+    out(kOutColor, g, k, dlg[k], cl[k]);
   }
   // SH: d rest_k = Y_k dlogit; the view direction's gradient reaches xyz
   // through dir = v / |v| (added to d_xyz below)
@@ -2185,22 +2207,22 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
     const float o = 1.f / (1.f + expf(-(kHot ? op_pre : a.g.opacity[(int64_t)g * a.g.opacity_stride])));
     dop = (dop * (1.f - o)) * o;
   }
-  out(kOutOpacity, (size_t)g, dop, op_pre);
+  out(kOutOpacity, g, 0, dop, op_pre);
   const bool any = dm0 != 0.f || dm1 != 0.f || G[0] != 0.f || G[1] != 0.f || G[2] != 0.f ||
                    G[3] != 0.f || acc[9] != 0.f;
   const bool raw = kHot || a.g.cov3d == nullptr;
   if (!any) {
     const float xv[3] = {xw, yw, zw};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) out(kOutXyz, 3 * (size_t)g + k, dxyz_sh[k], xv[k]);
+    for (int k = 0; k < 3; ++k) out(kOutXyz, g, k, dxyz_sh[k], xv[k]);
     if (raw) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) out(kOutScaling, 3 * (size_t)g + k, 0.f, scl_pre[k]);
+      for (int k = 0; k < 3; ++k) out(kOutScaling, g, k, 0.f, scl_pre[k]);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) out(kOutRotation, 4 * (size_t)g + k, 0.f, rot_pre[k]);
+      for (int k = 0; k < 4; ++k) out(kOutRotation, g, k, 0.f, rot_pre[k]);
     } else {
 #pragma unroll
-      for (int k = 0; k < 9; ++k) out(kOutCov, 9 * (size_t)g + k, 0.f, 0.f);
+      for (int k = 0; k < 9; ++k) out(kOutCov, g, k, 0.f, 0.f);
     }
     return;
   }
@@ -2269,7 +2291,7 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
     const float xv[3] = {xw, yw, zw};
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      out(kOutXyz, 3 * (size_t)g + j, (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ + (double)dxyz_sh[j]), xv[j]);
+      out(kOutXyz, g, j, (float)(R[j] * dX + R[4 + j] * dY + R[8 + j] * dZ + (double)dxyz_sh[j]), xv[j]);
   }
   float J[6], dV[4];
 #pragma unroll
@@ -2296,7 +2318,7 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
     for (int j = 0; j < 3; ++j) dS[i * 3 + j] = dot3(R[i], R[4 + i], R[8 + i], dCR[j], dCR[3 + j], dCR[6 + j]);
   if (!raw) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) out(kOutCov, 9 * (size_t)g + k, dS[k], 0.f);
+    for (int k = 0; k < 9; ++k) out(kOutCov, g, k, dS[k], 0.f);
     return;
   }
   // raw path: Sigma = M M^T, M = R(q) diag(s), s = exp(scaling), q = normalize(rotation)
@@ -2322,7 +2344,7 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
       dR[i * 3 + j] = dot3(Ss[i * 3], Ss[i * 3 + 1], Ss[i * 3 + 2], Rq[j], Rq[3 + j], Rq[6 + j]) * (s3[j] * s3[j]);
 #pragma unroll
   for (int j = 0; j < 3; ++j)  // dL/ds_j s_j: (dR / s_j) . Rq column j, times s_j
-    out(kOutScaling, 3 * (size_t)g + j, dot3(dR[j], dR[3 + j], dR[6 + j], Rq[j], Rq[3 + j], Rq[6 + j]), sc[j]);
+    out(kOutScaling, g, j, dot3(dR[j], dR[3 + j], dR[6 + j], Rq[j], Rq[3 + j], Rq[6 + j]), sc[j]);
   const float dw = 2.f * ((-z * dR[1] + y * dR[2]) + (z * dR[3] - x * dR[5]) + (-y * dR[6] + x * dR[7]));
   const float dx = 2.f * ((y * dR[1] + z * dR[2]) + (y * dR[3] - 2.f * x * dR[4]) + (-w * dR[5] + z * dR[6]) +
                           (w * dR[7] - 2.f * x * dR[8]));
@@ -2331,10 +2353,10 @@ __device__ __forceinline__ void project_bwd_one(const gs_project_bwd_args &a, in
   const float dz = 2.f * ((-2.f * z * dR[0] - w * dR[1]) + (x * dR[2] + w * dR[3]) + (-2.f * z * dR[4] + y * dR[5]) +
                           (x * dR[6] + y * dR[7]));
   const float dot = __builtin_fmaf(dw, w, __builtin_fmaf(dx, x, __builtin_fmaf(dy, y, dz * z)));
-  out(kOutRotation, 4 * (size_t)g + 0, (dw - w * dot) * iq, rq[0]);
-  out(kOutRotation, 4 * (size_t)g + 1, (dx - x * dot) * iq, rq[1]);
-  out(kOutRotation, 4 * (size_t)g + 2, (dy - y * dot) * iq, rq[2]);
-  out(kOutRotation, 4 * (size_t)g + 3, (dz - z * dot) * iq, rq[3]);
+  out(kOutRotation, g, 0, (dw - w * dot) * iq, rq[0]);
+  out(kOutRotation, g, 1, (dx - x * dot) * iq, rq[1]);
+  out(kOutRotation, g, 2, (dy - y * dot) * iq, rq[2]);
+  out(kOutRotation, g, 3, (dz - z * dot) * iq, rq[3]);
 }
 
 // kHot: partials present, no viewspace/conic cotangents, raw scale/rotation,
@@ -2363,10 +2385,14 @@ __global__ __launch_bounds__(kBlock) void k_project_bwd(gs_project_bwd_args a, F
       }
     }
   };
-  if constexpr (kAdam)
-    project_bwd_one<kHot>(a, g, sums, AdamOut(fa));
-  else
-    project_bwd_one<kHot>(a, g, sums, GradsOut{a});
+  if constexpr (kAdam) {
+    AdamOut out;
+    project_bwd_one<kHot>(a, g, sums, out);
+    out.flush(fa, g);
+  } else {
+    GradsOut out{a};
+    project_bwd_one<kHot>(a, g, sums, out);
+  }
 }
 
 // tile coordinates are packed in 12 bits (record word 11): images up to 65536 px a side

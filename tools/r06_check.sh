@@ -27,7 +27,8 @@ l = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print("C2", l["value"], "ms", l["ms_per_step"])
 PY
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > "$O/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$O/prof.log"; exit 1; }
-python3 "$R/tools/timed_kernel_stats.py" "$O/prof/run_kernel_trace.csv" 25 > "$O/kernel_stats_timed.txt" || true
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --diag-steps 0 --no-cpu-baseline > "$O/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$O/prof.log"; exit 1; }
+python3 "$R/tools/timed_kernel_stats.py" "$O/prof/run_kernel_trace.csv" 20 2 > "$O/kernel_stats_timed.txt" || true
+tail -1 "$O/kernel_stats_timed.txt"
 tail -1 "$O/prof.log" | cut -c1-300
 echo done
