@@ -107,7 +107,10 @@ def model(row_done, grid, res, peak, span, all_started, ty0, ty1, work_us):
 
 
 def main():
-    works = [float(x) for x in sys.argv[1:]] or [141.6, 176.0]
+    # each argument: work_us, or serial_us:overlapped_us (the tail kernels'
+    # cost in index order after the blend, and in band order during it)
+    works = [tuple(float(v) for v in x.split(":")) if ":" in x else (float(x), float(x)) for x in sys.argv[1:]] \
+        or [(141.6, 141.6)]
     npz = os.path.join(ROOT, "gpurun_out", "wave_times.npz")
     row_done, grid, res, peak, span, all_started = blend_rows(npz)
     ty0, ty1 = rects()
@@ -120,10 +123,12 @@ def main():
     print(f"idle GPU after every workgroup started: {(idle[after] * dt).sum():.1f} us x GPU "
           f"(of which before the last row completes: {(idle[after & (grid < row_done.max())] * dt).sum():.1f})")
     print(f"visible Gaussians with a rectangle: {len(ty0):,}; last row median {np.median(ty1):.0f}")
-    for wk in works:
-        t_overlap, t_serial, _ = model(row_done, grid, res, peak, span, all_started, ty0, ty1, wk)
-        print(f"tail work {wk:.1f} us: serial end {t_serial:.1f} us, overlapped end {t_overlap:.1f} us, "
-              f"saved {t_serial - t_overlap:.1f} us")
+    for ws, wo in works:
+        t_overlap, _, _ = model(row_done, grid, res, peak, span, all_started, ty0, ty1, wo)
+        t_serial = span + ws
+        print(f"tail work {ws:.1f} us after the blend (index order) vs {wo:.1f} us overlapped (band order): "
+              f"serial end {t_serial:.1f} us, overlapped end {t_overlap:.1f} us, saved {t_serial - t_overlap:.1f} us "
+              f"(before the band lists' own cost)")
 
 
 if __name__ == "__main__":
