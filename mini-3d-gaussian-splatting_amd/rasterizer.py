@@ -467,6 +467,9 @@ def _tile_layout(lib, buf, num_tiles: int, cam: CameraParams) -> _TileLayout:
 # below.  The two paths launch the same kernels on the same data: their
 # outputs and gradients are bit-identical (test_frame_entry_points_match).
 _FRAME_CALLS = os.environ.get("GS_FRAME_CALLS", "1") != "0"
+# gs_render_forward's patience with the counter poll before it synchronises the
+# stream and looks once more (0: the library's 10 s; tests shorten it)
+_POLL_TIMEOUT_MS = int(os.environ.get("GS_POLL_TIMEOUT_MS", "0"))
 _WS_BYTES: dict = {}  # (n, W, H, tile) -> gs_frame_workspace_bytes
 
 
@@ -569,6 +572,7 @@ def _forward_frame(cam: CameraParams, xyz, cov3d, scaling, rotation, logits, opa
     hc.seq = hc.seq % 0x7FFFFFFF + 1
     fa.host_counters_dev, fa.host_counters_host, fa.host_seq = hc.dptr, hc.t.data_ptr(), hc.seq
     fa.pair_counts, fa.pix_neval = N.ptr(pair_counts), N.ptr(pix_neval)
+    fa.poll_timeout_ms = _POLL_TIMEOUT_MS
     st = lib.gs_render_forward(C.byref(fa), s)
     if st == N.GS_RETRY_FULL_KEYS:
         # a visible depth outside the window, or an MSD bucket over capacity

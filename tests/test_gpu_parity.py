@@ -1241,3 +1241,54 @@ def test_concurrent_renders_two_threads(pkg, cuda):
         assert len(got[i]) == 6
         for img in got[i]:
             assert torch.equal(img, want[i]), i
+
+
+def test_frame_poll_timeout_synchronises_before_failing(pkg, cuda):
+    """gs_render_forward's counter poll gives up after its
+    patience (here 1 ms) only after synchronising the stream and reading the
+    word once more -- a healthy stream with a long queue ahead of the count
+    renders normally (the same image as without the queue)."""
+    RZ = pkg.rasterizer
+    sc = pkg.synthetic.make_scene(20000, 320, 240, seed=4)
+    m = pkg.synthetic.to_model(sc, pkg.GaussianModel, cuda)
+    st = pkg.RenderSettings(240, 320, torch.tensor([0.1, 0.2, 0.3]))
+    cam = Cam(320, 240, sc.fovx, sc.fovy)
+    with torch.no_grad():
+        ref = pkg.GaussianRenderer().render(cam, m, st)["image"].clone()
+        saved = RZ._POLL_TIMEOUT_MS
+        try:
+            RZ._POLL_TIMEOUT_MS = 1
+            a = torch.randn(4096, 4096, device=cuda)
+            for _ in range(40):  # tens of ms of work queued ahead of the frame's count
+                a = a @ a
+                a = a / a.abs().max()
+            out = pkg.GaussianRenderer().render(cam, m, st)["image"]
+        finally:
+            RZ._POLL_TIMEOUT_MS = saved
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+def test_second_backward_of_one_frame(pkg, cuda):
+    """a second backward over the same frame
+    (retain_graph=True) clears the slot flags the first one left, at the
+    default tile (frame entry points) and at a tile replayed in cell batches
+    (stage path): the gradients accumulate to exactly twice the first."""
+    RZ = pkg.rasterizer
+    sc = pkg.synthetic.make_scene(3000, 96, 72, seed=6, sigma_range=(0.005, 0.03))
+    saved = RZ.PARTIAL_BUDGET_BYTES
+    try:
+        for tile, budget in ((16, saved), (64, 41 * 2000 * 8)):
+            RZ.PARTIAL_BUDGET_BYTES = budget
+            m = pkg.synthetic.to_model(sc, pkg.GaussianModel, cuda)
+            out = pkg.GaussianRenderer(tile_size=tile).render(Cam(96, 72, sc.fovx, sc.fovy), m,
+                                                             pkg.RenderSettings(72, 96, torch.tensor([0.1, 0.2, 0.3])))
+            loss = out["image"].sum() + out["alpha"].mean()
+            loss.backward(retain_graph=True)
+            first = [p.grad.clone() for p in m.grad_parameters() if p.grad is not None]
+            loss.backward()
+            second = [p.grad for p in m.grad_parameters() if p.grad is not None]
+            for a_, b_ in zip(first, second):
+                assert torch.equal(b_, a_ * 2), tile
+    finally:
+        RZ.PARTIAL_BUDGET_BYTES = saved
