@@ -200,7 +200,8 @@ typedef struct gs_bin_args {
   int32_t n;
   int32_t tiles_x, tiles_y;
   const uint32_t *sorted_ids; /* [n] depth-sorted Gaussian ids (visible first) */
-  const uint32_t *rects;      /* [n,2] from gs_project_forward */
+  const uint32_t *rects;      /* [n,2] from gs_project_forward (cleared by gs_bin_emit of a failed
+                                 device-resident frame, see device_counts) */
   const uint8_t *vis;         /* [n]   from gs_project_forward */
   uint32_t *counters;         /* [GS_NUM_COUNTERS] */
   const uint32_t *key_minmax; /* gs_project_args.key_minmax (reduced into counters[2..3]) */
@@ -230,6 +231,10 @@ typedef struct gs_bin_args {
   int32_t key_bits;        /* 0: no window check */
   uint32_t *step_flags;    /* optional device word: the status is ORed into it (sticky until the caller
                               clears it; gs_adam_args.skip_flag reads it) */
+  int32_t device_counts;   /* a device-resident frame (gs_render_fwd_args.device_counts): when the
+                              status is non-zero, gs_bin_emit emits nothing and clears every
+                              rectangle (rects), so that the frame's backward gathers zero slots --
+                              none past the capacity -- and the caller redoes the frame */
   uint32_t *frame_seq;     /* optional device word: incremented by every gs_bin_count; its new value is
                               written to host_counters[4] in place of host_seq (a captured graph
                               replays one frame per value).  host_counters also gets [5] the status,
@@ -396,8 +401,6 @@ typedef struct gs_project_bwd_args {
   float *grad_sums;            /* [n, GS_PAIR_GRAD_FLOATS]: g's partials summed (written first when
                                   pair_grads is given, else read as is); NULL: no blend gradient */
   int32_t partial_groups;      /* G of pair_grads / slot_live: the blend backward's cell_count */
-  const uint32_t *frame_status; /* optional device word (counters[4]): non-zero -> the gather writes
-                                  zero sums (a device-resident frame that failed reads no partials) */
 } gs_project_bwd_args;
 gs_status gs_project_backward(const gs_project_bwd_args *a, gs_stream_t stream);
 /* The gather alone: grad_sums[g] = (accumulate ? grad_sums[g] : 0) + the sum
@@ -613,7 +616,7 @@ typedef struct gs_render_bwd_args {
   void *blend_events[2];           /* optional hipEvent_t pair, recorded on the stream right before and
                                       after the blend backward launch(es): its time alone (profiling) */
   int32_t device_counts;           /* the forward was device-resident: M, T are not read; pair_grads holds
-                                      capacity * flag_groups partials; the gather reads the frame status */
+                                      capacity * flag_groups partials (a failed frame gathers zero slots) */
   const gs_adam_args *fused_adam;  /* with project = 1: gs_project_backward_adam with these tensors (no
                                       d_* written), or NULL: the plain projection backward */
 } gs_render_bwd_args;

@@ -70,7 +70,8 @@ class GsBinArgs(C.Structure):
         ("workspace_bytes", C.c_size_t),
         ("tile_keys", _vp), ("pair_gauss", _vp), ("pair_offset", _vp), ("records", _vp),
         ("capacity", C.c_int64), ("host_counters", _vp), ("host_seq", C.c_uint32),
-        ("key_base", C.c_uint32), ("key_bits", C.c_int32), ("step_flags", _vp), ("frame_seq", _vp),
+        ("key_base", C.c_uint32), ("key_bits", C.c_int32), ("step_flags", _vp), ("device_counts", C.c_int32),
+        ("frame_seq", _vp),
     ]
 
 
@@ -106,7 +107,7 @@ class GsProjectBwdArgs(C.Structure):
         ("rects", _vp), ("pair_offset", _vp), ("order", _vp), ("pair_grads", _vp), ("g_means2d", _vp),
         ("g_conics", _vp), ("d_xyz", _vp), ("d_cov3d", _vp), ("d_scaling", _vp),
         ("d_rotation", _vp), ("d_color_logits", _vp), ("d_opacity", _vp), ("d_sh_rest", _vp),
-        ("slot_live", _vp), ("grad_sums", _vp), ("partial_groups", C.c_int32), ("frame_status", _vp),
+        ("slot_live", _vp), ("grad_sums", _vp), ("partial_groups", C.c_int32),
     ]
 
 

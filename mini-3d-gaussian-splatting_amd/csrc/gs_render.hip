@@ -197,6 +197,7 @@ gs_status gs_render_forward(gs_render_fwd_args *a, gs_stream_t stream) {
   ba.key_bits = a->key_bits;
   ba.step_flags = a->step_flags;
   ba.frame_seq = a->frame_seq;
+  ba.device_counts = dev ? 1 : 0;
   if (!a->resume) {
     a->M = a->T = 0;
     a->depth_min_bits = 0xFFFFFFFFu;
@@ -376,7 +377,8 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
   if (dev && (a->fb.capacity <= 0 || G < cells))
     return gs_internal_fail(GS_ERR_INVALID_ARG, "%s: device_counts needs the forward's capacity and one batch", what);
   // (device-resident: T unknown here -- the blend backward is launched over
-  // every tile, reads the ranges T_eff made, and the gather the frame status)
+  // every tile and reads the ranges T_eff made; a failed frame's emission
+  // cleared the rectangles, so its gather reads no slot)
   const bool pixel_grads = (dev || (a->M > 0 && a->T > 0)) && a->g_image;
   const int32_t T = dev ? (int32_t)a->fb.capacity : a->T;
   if (pixel_grads) {
@@ -418,7 +420,6 @@ gs_status gs_render_backward(gs_render_bwd_args *a, gs_stream_t stream) {
     ga.pair_grads = a->pair_grads;
     ga.slot_live = flags;
     ga.grad_sums = grad_sums;
-    ga.frame_status = dev ? reinterpret_cast<const uint32_t *>(fw + F.counters) + 4 : nullptr;
     hipEvent_t ev0 = (hipEvent_t)a->blend_events[0], ev1 = (hipEvent_t)a->blend_events[1];
     if (ev0 && record_event(ev0, stream) != hipSuccess)
       return gs_internal_fail(GS_ERR_LAUNCH, g_event_err, what);

@@ -1077,11 +1077,22 @@ __global__ __launch_bounds__(kBlock) void k_bin_emit(gs_bin_args a, const uint32
   __shared__ uint32_t s_tmp3[3][kBlock / kWave];
   __shared__ uint8_t s_owner[kOwnerCap];
   __shared__ uint32_t s_hist[kHist ? kHistSpan * kRadix : 1];
+  const long long base = (long long)blockIdx.x * kBinChunk;
+  // a device-resident frame that failed (gs_bin_count's status): no entry is
+  // emitted and every rectangle of the chunk is cleared, so the frame's
+  // backward gathers zero slots per Gaussian -- never a slot past the
+  // capacity (the caller redoes the frame on the host path)
+  if (a.device_counts && a.counters[4] != 0u) {
+    for (int r = 0; r < kBinChunk / kBlock; ++r) {
+      const long long g = base + r * kBlock + threadIdx.x;
+      if (g < a.n) reinterpret_cast<uint2 *>(const_cast<uint32_t *>(a.rects))[g] = make_uint2(1u, 1u);
+    }
+    return;
+  }
   // T entries do not fit: do nothing (the caller re-emits into T-sized
   // buffers; the slot pass below is not idempotent, so it must run once)
   const uint32_t T = a.counters[1];
   if ((long long)T > a.capacity) return;
-  const long long base = (long long)blockIdx.x * kBinChunk;
   uint32_t out_base = partials[blockIdx.x];
   // first-pass digit counts of the entries this block writes: sort block
   // (out_base + o) / kSortChunk, digit key & hmask (shift 0)
@@ -1963,7 +1974,13 @@ constexpr int kF2 = GS_PAIR_GRAD_FLOATS / 2;
 #define GS_GATHER_NB 3
 #endif
 constexpr int kGatherNB = GS_GATHER_NB;
-template <int QL, int HL, int kNG>
+// Gather mode (compile time: a runtime test costs the latency-bound gather
+// ~5 us at C3, measured for a status word's scalar load on every wave's path):
+// kGatherOrder -- the Gaussians walked in gs_project_bwd_args.order.  (A
+// failed device-resident frame needs no test here: its emission cleared the
+// rectangles, so every Gaussian gathers zero slots, gs_bin_args.device_counts.)
+constexpr int kGatherOrder = 2;
+template <int QL, int HL, int kNG, int kMode>
 __device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint32_t ng, long long t, int g,
                                              float2 acc[kF2]) {
   constexpr int LPG = QL * HL;
@@ -1981,9 +1998,7 @@ __device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint3
   unpack_rect(a.rects, gi, tx0, tx1, ty0, ty1);
   uint32_t off32 = a.pair_offset[gi];
   asm volatile("" : "+v"(off32));
-  // (a device-resident frame that failed has no partials to read: zero sums)
-  const bool frame_ok = !a.frame_status || *a.frame_status == 0u;
-  const uint32_t cnt = (valid && visb && frame_ok) ? rect_touches(tx0, tx1, ty0, ty1) : 0u;
+  const uint32_t cnt = (valid && visb) ? rect_touches(tx0, tx1, ty0, ty1) : 0u;
   // lane q sums partial groups q, q + QL, ... of a slot's ng (one pass when ng <= QL)
   for (uint32_t qc = (uint32_t)q; cnt > (uint32_t)h && qc < ng; qc += QL) {
     const size_t off = off32;
@@ -2037,14 +2052,14 @@ __device__ __forceinline__ void gather_slots(const gs_project_bwd_args &a, uint3
 
 // accumulate: grad_sums = grad_sums + this batch's sums (the cell batches of
 // one backward, added in batch order: deterministic), else grad_sums = them.
-template <int QL, int HL, int kNG = 0>  // kNG > 0: the partial groups per slot at compile time (else ng)
+template <int QL, int HL, int kNG = 0, int kMode = 0>  // kNG > 0: the partial groups per slot at compile time (else ng)
 __global__ __launch_bounds__(kBlock) void k_gather_slots(gs_project_bwd_args a, uint32_t ng_rt, int accumulate) {
   constexpr int LPG = QL * HL;
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   int g = (int)(t / LPG);
-  if (a.order && g < a.g.n) g = (int)a.order[g];  // (a walk in another order: gs_project_bwd_args.order)
+  if ((kMode & kGatherOrder) && g < a.g.n) g = (int)a.order[g];  // (gs_project_bwd_args.order)
   float2 acc[kF2];
-  gather_slots<QL, HL, kNG>(a, kNG > 0 ? (uint32_t)kNG : ng_rt, t, g, acc);
+  gather_slots<QL, HL, kNG, kMode>(a, kNG > 0 ? (uint32_t)kNG : ng_rt, t, g, acc);
   if ((t % LPG) == 0 && g < a.g.n) {
     float2 *out = reinterpret_cast<float2 *>(a.grad_sums) + (size_t)g * kF2;
     if (accumulate) {
@@ -2820,6 +2835,13 @@ gs_status gs_blend_backward_lane_stats(const gs_blend_bwd_args *a, uint64_t *his
 namespace {
 gs_status launch_gather(const gs_project_bwd_args *a, int accumulate, hipStream_t s) {
   const uint32_t ng = (uint32_t)a->partial_groups;
+  const unsigned gb = div_up(8LL * a->g.n, kBlock);
+  if (a->order) {  // (a walk in another order: the default tile only, a probe's)
+    if (ng != 4)
+      return fail(GS_ERR_UNSUPPORTED, "%s: order needs the default tile's 4 partial groups", "gs_gather_partials");
+    k_gather_slots<4, 2, 4, kGatherOrder><<<gb, kBlock, 0, s>>>(*a, ng, accumulate);
+    return check_launch("gs_gather_partials");
+  }
   if (ng == 1)
     k_gather_slots<1, kGatherHL1><<<div_up((long long)kGatherHL1 * a->g.n, kBlock), kBlock, 0, s>>>(*a, ng, accumulate);
   else if (ng == 2)
