@@ -15,7 +15,9 @@ for f in glob.glob(root + "/p*/pmc_counter_collection.csv"):
         k = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"]).split("(")[0].replace("void ", "")
         # template arguments dropped (k_blend_fwd<false, true> -> k_blend_fwd), except the
         # measurement-only counting forward, kept apart
-        k = "k_blend_fwd_counting" if k.startswith("k_blend_fwd<true") else re.sub(r"<.*", "", k)
+        # and the projection backward with the Adam update fused in (the replayed step's) apart from the plain one
+        k = ("k_blend_fwd_counting" if k.startswith("k_blend_fwd<true") else
+             "k_project_bwd_adam" if k.startswith("k_project_bwd<true, true>") else re.sub(r"<.*", "", k))
         if keep and not any(s in k for s in keep):
             continue
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))

@@ -16,6 +16,7 @@ import sys
 
 PEAK = 8000.0  # GB/s (HBM3E spec)
 SORT_CHUNK = 2048  # radix sort block (gs_internal.h kSortBlockEntries)
+ALIAS = {"k_tile_ranges4": "k_tile_ranges"}  # (four positions per thread at the default tile: the same model)
 
 
 def counts_from_bench(line: dict) -> dict:
@@ -36,8 +37,11 @@ def bench_line(path: str) -> dict:
     raise ValueError(f"no bench JSON line in {path}")
 
 
-def model(k: dict) -> dict:
-    """kernel -> (launches per step, algorithmic bytes per step, model text)."""
+def model(k: dict, fused_adam: bool = False) -> dict:
+    """kernel -> (launches per step, algorithmic bytes per step, model text).
+    fused_adam: the replayed step's projection backward applies the Adam update
+    itself (gs_project_backward_adam): no gradient written or re-read, the
+    moments and the updated parameters moved there, no k_adam launch."""
     N, M, T, R, L, HW, TILES = (k[x] for x in ("N", "M", "T", "R", "L", "HW", "TILES"))
     nb_n, nb_t = -(-N // SORT_CHUNK), -(-T // SORT_CHUNK)
     return {
@@ -57,7 +61,10 @@ def model(k: dict) -> dict:
                                                       "40 B/G written"),
         "k_project_bwd": (1, 196 * N, "40 B/G sums + ~100 B/G read, 56 B/G written"),
         "k_adam": (1, 392 * N, "14 floats/G x (param, m, v, grad read + param, m, v written)"),
-    }
+        "k_project_bwd_adam": (1, 420 * N, "40 B/G sums + ~100 B/G read; Adam fused: 14 floats/G x (m, v read + "
+                                           "param, m, v written)"),
+    } if not fused_adam else {k: v for k, v in model(k, False).items() if k not in ("k_project_bwd", "k_adam")} | {
+        "k_project_bwd_adam": model(k, False)["k_project_bwd_adam"]}
 
 
 def pmc(path):
@@ -66,7 +73,7 @@ def pmc(path):
         if line.startswith("#"):
             continue
         if not line.startswith(" "):
-            cur = line.strip()
+            cur = ALIAS.get(line.strip(), line.strip())
             out[cur] = {}
         elif cur:
             k, v = line.split()
@@ -80,6 +87,9 @@ def timed(path):
         m = re.match(r"(k_\w+)(<[^>]*>)?\s+(\d+)\s+([\d.]+)", line)
         if m:
             k = m.group(1)
+            if k == "k_project_bwd" and (m.group(2) or "").replace(" ", "") == "<true,true>":
+                k = "k_project_bwd_adam"  # (the projection backward with the Adam update fused in)
+            k = ALIAS.get(k, k)
             calls, avg = int(m.group(3)), float(m.group(4))
             tot = out.get(k, (0, 0.0))
             out[k] = (tot[0] + calls, tot[1] + calls * avg)
@@ -91,7 +101,8 @@ def table(p: dict, t: dict, counts: dict) -> str:
              f"{'kernel':20s} {'launch/step':>11s} {'us/step':>8s} {'alg MB':>8s} {'PMC MB':>8s} {'raw MB':>8s} "
              f"{'alg GB/s':>9s} {'frac':>6s} {'PMC/alg':>7s}  model"]
     tot_us = tot_alg = 0.0
-    for k, (n, alg, text) in model(counts).items():
+    fused = "k_project_bwd_adam" in t  # (the replayed step with the optimizer in the backward)
+    for k, (n, alg, text) in model(counts, fused).items():
         if k not in t or k not in p:
             continue
         us = t[k] * n
