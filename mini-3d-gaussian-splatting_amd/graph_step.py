@@ -66,6 +66,9 @@ class GraphedStep:
                  optimizer=None, eager_step: Optional[Callable[[], None]] = None, fused_adam: bool = False):
         if not getattr(model, "_gs_fused_covariance", False):
             raise ValueError("GraphedStep renders this package's GaussianModel (raw scaling / rotation)")
+        if optimizer is not None and not hasattr(optimizer, "param_out"):
+            raise TypeError("GraphedStep replays FusedAdam's update (optim.FusedAdam), got "
+                            f"{type(optimizer).__name__}")
         self.renderer, self.camera, self.model, self.settings, self.optimizer = (renderer, camera, model, settings,
                                                                                  optimizer)
         self.cam = camera_params(camera, settings, renderer.radius_min, renderer.radius_max, renderer.tile_size)
