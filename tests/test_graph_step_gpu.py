@@ -154,3 +154,57 @@ def test_fused_adam_in_the_projection_backward(pkg, cuda):
         assert len(gs.redone) == 1 and gs.redone[0][0] & pkg._native.GS_FRAME_NEED_CAPACITY
         _assert_same_state(ma, oa, mb, ob)
         gs.close()
+
+
+@pytest.mark.parametrize("size", ["C2", "C3"])
+def test_graph_replay_at_benchmark_size(pkg, cuda, size):
+    """The capacity-sized launches at the BASELINE sizes (C2: 100k Gaussians,
+    800x800; C3: 1M, 1920x1080, T = 4.4M list entries): three replayed steps
+    with the optimizer in the backward and shadow parameter outputs (the
+    bench's step) equal three eager steps bit for bit -- parameters, moments,
+    and the last frame's image, alpha, depth."""
+    n, w, h = {"C2": (100_000, 800, 800), "C3": (1_000_000, 1920, 1080)}[size]
+    res = []
+    for graph in (False, True):
+        scene = pkg.synthetic.make_scene(n, w, h, seed=0)
+        model = pkg.synthetic.to_model(scene, pkg.GaussianModel, cuda)
+        opt = pkg.optim.FusedAdam([{"params": [model._xyz], "lr": 1.6e-4},
+                                   {"params": [model._features_dc], "lr": 2.5e-3},
+                                   {"params": [model._opacity], "lr": 0.05}, {"params": [model._scaling], "lr": 5e-3},
+                                   {"params": [model._rotation], "lr": 1e-3}])
+        for p in model.grad_parameters():
+            opt.set_output(p, torch.empty_like(p))
+
+        class Cam:
+            _width, _height, _FoVx, _FoVy = w, h, scene.fovx, scene.fovy
+
+            def world_view_transform(self):
+                return torch.eye(4)
+        st = pkg.RenderSettings(image_height=h, image_width=w, bg_color=torch.zeros(3))
+        g = torch.Generator().manual_seed(1)
+        cot = [(torch.rand(s, generator=g) * 2 - 1).to(cuda) for s in ((3, h, w), (1, h, w), (1, h, w))]
+        if graph:
+            gs = pkg.GraphedStep(pkg.GaussianRenderer(), Cam(), model, st, cot, opt, fused_adam=True)
+            with torch.cuda.stream(gs.stream):
+                for _ in range(4):
+                    gs.step()
+            gs.finish()
+            assert gs.redone == [] and gs.replays == 3
+            imgs = (gs.image.clone(), gs.alpha.clone(), gs.depth.clone())
+            gs.close()
+        else:
+            out = _eager(pkg, model, opt, Cam(), st, cot, 4)
+            imgs = tuple(out[k].detach().clone() for k in ("image", "alpha", "depth"))
+        state = [(opt.param_out[p].clone(), opt.state[p]["exp_avg"].clone(), opt.state[p]["exp_avg_sq"].clone(),
+                  opt.state[p]["step"]) for p in model.grad_parameters() if p in opt.state]
+        res.append((imgs, state))
+        del model, opt
+        torch.cuda.empty_cache()
+    (ia, sa), (ib, sb) = res
+    for x, y in zip(ia, ib):
+        assert torch.equal(x, y)
+    assert len(sa) == len(sb) == 5
+    for a_, b_ in zip(sa, sb):
+        assert a_[3] == b_[3]
+        for x, y in zip(a_[:3], b_[:3]):
+            assert torch.equal(x, y)
