@@ -265,9 +265,10 @@ gs_status gs_tile_ranges(const gs_range_args *a, gs_stream_t stream);
  * compositing of its tile's list, termination once A >= 0.995, background
  * composite (bg counted twice, as the reference does), clamps, depth
  * normalisation.  One 64-lane workgroup per (tile, 8x8 cell), the cells of
- * a tile independent of each other, each walking the tile's list.  pix_state
- * keeps what the backward needs: [H*W] float4 (acc_r, acc_g, acc_b, D) and
- * [H*W] float2 (A, bits of n_eval). */
+ * a tile independent of each other, each walking the tile's list.  What the
+ * backward needs beside the outputs themselves: pix_flags (one byte per
+ * pixel: which clamps blocked), cell_neval (per cell, the evaluated prefix)
+ * and the liveness bitmap. */
 typedef struct gs_blend_fwd_args {
   gs_camera cam;
   int32_t tiles_x, tiles_y;
