@@ -2511,7 +2511,7 @@ bool cam_ok(const gs_camera &c) {
   if (c.tile_size < 1 || c.tile_size > GS_MAX_TILE || c.image_width <= 0 || c.image_height <= 0) return false;
   return div_up(c.image_width, c.tile_size) <= GS_MAX_TILES_AXIS && div_up(c.image_height, c.tile_size) <= GS_MAX_TILES_AXIS;
 }
-const char *kCamMsg = "%s: tile_size must be in [1, 4096], the image non-empty with at most 4096 tiles per axis";
+const char *kCamMsg = "%s: tile_size must be in [1, 32768], the image non-empty with at most 4096 tiles per axis";
 
 // A Gaussian's rectangle is at most 2 floor(r) + 1 <= 2 floor(radius_max) + 1
 // pixels wide (renderer.py:278-293), clipped to the image: its tile width

@@ -816,6 +816,21 @@ def test_large_tiles_vs_oracle(pkg, cuda, tile):
     assert not errs, errs
 
 
+@pytest.mark.parametrize("tile", [4150, 10 ** 6])
+def test_wide_image_large_tiles_vs_oracle(pkg, cuda, tile):
+    """Tile edges above 4096 px (GS_MAX_TILE is 32768 since round 6): a
+    4200 x 40 image in two tiles of 4150 px (the second 50 px wide), and
+    tile_size above the image, rendered as one tile of 4200 px -- both as the
+    reference's binning (renderer.py:261-298).  519^2 / 525^2 cells per tile:
+    the backward replays them in memory-bounded batches."""
+    W, H = 4200, 40
+    sc = pkg.synthetic.make_scene(2500, W, H, seed=53)
+    errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.2, 0.1, 0.0), renderer_kw=dict(tile_size=tile),
+                                    label=f"wide tile{tile}")
+    assert bad.sum() <= 2
+    assert not errs, errs
+
+
 def test_wide_rects_vs_oracle(pkg, cuda):
     """radius_max far above the default: rectangles up to 101 x 76 tiles of
     4 px, so a round of 256 Gaussians emits ~1M entries through many windows
