@@ -1590,16 +1590,8 @@ struct BwdStats {
   uint32_t *per_group;       // [grid][4]
 };
 
-#ifndef GS_BWD_WAVES
-#define GS_BWD_WAVES 0
-#endif
-#if GS_BWD_WAVES
-#define GS_BWD_OCC __attribute__((amdgpu_waves_per_eu(GS_BWD_WAVES)))
-#else
-#define GS_BWD_OCC
-#endif
 template <bool kT16, bool kStats = false>
-__global__ __launch_bounds__(kWave) GS_BWD_OCC void k_blend_bwd(gs_blend_bwd_args a, BwdStats stats = {nullptr, nullptr}) {
+__global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdStats stats = {nullptr, nullptr}) {
   __shared__ float2 s_dc[kBwdGroup][kBwdRow];  // per group entry and pixel: (dop, c)
   __shared__ uint32_t s_hist[kStats ? 2 * 65 : 1];
   uint32_t n_rep = 0, n_rep32 = 0, sum_run = 0, sum_con = 0;  // (kStats)
