@@ -48,6 +48,10 @@ constexpr float kAlphaStop = 0.995f;             // renderer.py:352
 // already disagree -- and it saves the compare on w for every evaluated
 // pair (C3: the same 9 knife-edge pixels).  Forward and backward share it.
 constexpr float kSkipS = 23.0258509f;
+// The blend kernels evaluate t = -s/2 directly: the conic coefficients are
+// staged as -Q/2 (a power-of-two scaling, exact for every product and sum of
+// the reference's s), so the skip is t < -ln(1e5), the same decision.
+constexpr float kSkipT = -0.5f * kSkipS;
 
 thread_local char g_err[512];
 
@@ -93,32 +97,35 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) {
 typedef float f4_u8 __attribute__((ext_vector_type(4), aligned(8)));
 typedef float f2_u8 __attribute__((ext_vector_type(2), aligned(8)));
 
-// exp(x) for the blend's range x in [-11.6, 0] (it evaluates exp(-s/2) only
-// for s <= 23.1): x*log2(e) split into ph + pl (Cody-Waite, as ocml's expf),
-// then 2^ph by v_exp_f32 corrected by (1 + pl ln2) -- no range reduction and
-// ldexp, since 2^ph stays a normal float here.  ~1 ulp, like expf; forward
-// and backward share it, so their decisions replay bit-identically (C3:
-// the same 9 knife-edge pixels vs the oracle as the full expf sequence).
-// Dropping the log2(e) low-part term saves a VALU per evaluated pair (-20 us
-// per C3 step) but is <= 3 ulp at x = -11.6: 12 knife-edge pixels and the
-// scaling gradient's error 5.4e-4 -> 1.2e-3 of scale.  Not taken.
-__device__ __forceinline__ float exp_inrange(float x) {
-  const float ph = x * 0x1.715476p+0f;
-  float pl = __builtin_fmaf(x, 0x1.715476p+0f, -ph);
-  pl = __builtin_fmaf(x, 0x1.4ae0bep-26f, pl);
+// exp(t) for the blend's exponent t = -s/2 (it evaluates the exp only for
+// s <= 23.1, t in [-11.6, 0]; beyond, for non-positive-definite conics, it
+// stays finite until 2^ph overflows), given t itself: the blend kernels
+// compute t from the conic staged as -Q/2 (stage_conic0/1).  ph = t log2(e)
+// rounded, 2^ph by v_exp_f32 (no range reduction or ldexp: 2^ph stays a
+// normal float here), times (1 + d) with the remainder d = t - ph ln2 in
+// natural-log units (Cody-Waite: ln2 in two parts, each fma's product exact).
+// ~1 ulp, like expf; forward and backward share it, so their decisions
+// replay bit-identically.  5 VALU per pair.  Rounds 2-5 took the remainder
+// in log2 units (ph + pl from x log2(e), then 2^ph (1 + pl ln2)) and the
+// exponent from s (x = -s/2): 6 VALU, and the same values (round 6: every one
+// of 2.6 M sampled t, emulated).  Dropping the remainder's low part instead
+// saves a VALU too, but is <= 3 ulp at t = -11.6: 12 knife-edge pixels and
+// the scaling gradient's error 5.4e-4 -> 1.2e-3 of scale (round 2).  Not taken.
+__device__ __forceinline__ float exp_blend(float t) {
+  const float ph = t * 0x1.715476p+0f;
   const float r = __builtin_amdgcn_exp2f(ph);
-  return __builtin_fmaf(r, pl * 0x1.62e430p-1f, r);
+  float d = __builtin_fmaf(-ph, 0x1.62e430p-1f, t);
+  d = __builtin_fmaf(-ph, -0x1.05c610p-29f, d);
+  return __builtin_fmaf(r, d, r);
 }
 
-// exp(-s/2) for s in [0, 23.1]: exp_inrange(-0.5f * s) with the -1/2 folded
-// into the constants -- scaling by a power of two is exact, so every product
-// (and each fma's exact product) is the same real number: bit-identical.
-__device__ __forceinline__ float exp_neg_half(float s) {
-  const float ph = s * -0x1.715476p-1f;
-  float pl = __builtin_fmaf(s, -0x1.715476p-1f, -ph);
-  pl = __builtin_fmaf(s, -0x1.4ae0bep-27f, pl);
-  const float r = __builtin_amdgcn_exp2f(ph);
-  return __builtin_fmaf(r, pl * 0x1.62e430p-1f, r);
+// A record's conic staged for the blend loops as -Q/2: t = conic_s(dx, dy,
+// h00, ho, h11) is then -s/2 exactly.
+__device__ __forceinline__ float4 stage_conic0(float4 r0) {  // (mx, my, q00, q11) -> (mx, my, h00, h11)
+  return make_float4(r0.x, r0.y, -0.5f * r0.z, -0.5f * r0.w);
+}
+__device__ __forceinline__ float4 stage_conic1(float4 r1) {  // (qo, o, r, g) -> (ho, o, r, g)
+  return make_float4(-0.5f * r1.x, r1.y, r1.z, r1.w);
 }
 
 // s = [dx dy] Q [dx dy]^T for the blend's conic form (q00, qo = Q01+Q10,
@@ -1438,8 +1445,8 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
     if (!wave_any(A < kAlphaStop)) break;  // every pixel of the cell done
     // stage the batch (this wave's own earlier reads precede these writes)
     float4 *d = reinterpret_cast<float4 *>(&s_rec[6 * lane]);
-    d[0] = n0;
-    d[1] = n1;
+    d[0] = stage_conic0(n0);  // (the conic as -Q/2: the loop computes t = -s/2)
+    d[1] = stage_conic1(n1);
     d[2] = n2;
     const bool hit = b + (uint32_t)lane < end && cell_hit(n0.x, n0.y, n0.z, n1.x, n0.w, (float)x0, (float)y0);
     const unsigned long long mw = __builtin_amdgcn_ballot_w64(hit);
@@ -1456,6 +1463,8 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged records, for every lane
     unsigned long long livem = 0;  // entries some lane of this cell evaluated
+    // (packing the hits at compile-time offsets, round 6, so that the loop
+    // needs no per-entry address move: no change, profiles/r06/exp5/)
     while (m) {
       const uint32_t bit = (uint32_t)__builtin_ctzll(m);
       m &= ~(1ull << bit);
@@ -1464,10 +1473,10 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
       const float2 *rj = reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(s_rec) + ja);
       const float2 pm = lds_pair(rj), pq = lds_pair(rj + 1), po = lds_pair(rj + 2);
       const float dx = fx - pm.x, dy = fy - pm.y;
-      const float s = conic_s(dx, dy, pq.x, po.x, pq.y);  // :333
+      const float t = conic_s(dx, dy, pq.x, po.x, pq.y);  // -s/2 (:333; conic staged as -Q/2)
       const bool run = A < kAlphaStop;
       const unsigned long long rm = __builtin_amdgcn_ballot_w64(run);  // (the compare's own SGPR result)
-      const bool lv = run && !(s > kSkipS);  // the :336 skip, decided on s
+      const bool lv = run && !(t < kSkipT);  // the :336 skip, decided on s
       if (wave_any(lv)) {
         livem |= 1ull << bit;
         if (rm != runm) {  // lanes stopped since the last evaluated entry (rare)
@@ -1476,7 +1485,7 @@ __global__ __launch_bounds__(kWave) void k_blend_fwd(gs_blend_fwd_args a) {
           runm = rm;
         }
         last = b - start + bit + 1;
-        const float w = sat01(exp_neg_half(s));          // :334
+        const float w = sat01(exp_blend(t));             // :334
         const float ai = lv ? sat01(po.y * w) : 0.f;      // :339 (skips folded into the weight)
         const float c = (1.f - A) * ai;                   // :343-344
         const float2 prg = lds_pair(rj + 3), pbz = lds_pair(rj + 4);
@@ -1713,8 +1722,9 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
     const int j = lane / kBwdLanes, col = lane % kBwdLanes;
     if (j < k) {
       const uint32_t e = (uint32_t)j;
-      const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * e];  // mx my q00 q11
-      const float2 ib = s_wrec[6 * e + 2];                                // qo o
+      const float4 ia = reinterpret_cast<const float4 *>(s_wrec)[3 * e];  // mx my h00 h11 (h = -q/2)
+      const float2 ib = s_wrec[6 * e + 2];                                // ho o
+      const float q00 = -2.f * ia.z, q11 = -2.f * ia.w, qo = -2.f * ib.x;  // (exact)
       const uint32_t slot = __float_as_uint(s_wrec[6 * e + 5].x);
       const float hop = -0.5f * ib.y;
       // this lane's pixels (x0 + col, y0 + r): dx = bx, dy = by + (r - rc).
@@ -1726,8 +1736,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
       // 1.7e-4 of the tensor's scale measured on a sub-pixel Gaussian (2e-6
       // recentred).  Always recentring cost +28 us per C3 step, this test +7.
       const float bx = (float)(x0 + col) - ia.x;
-      const float q01h = 0.5f * ib.x;
-      const bool small_y = ia.z < 4.f * (ia.z * ia.w - q01h * q01h);  // Sigma_yy = q00 / det < 4
+      const float q01h = 0.5f * qo;
+      const bool small_y = q00 < 4.f * (q00 * q11 - q01h * q01h);  // Sigma_yy = q00 / det < 4
       float S0 = 0.f, Soy = 0.f, Soyy = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
       float rc = 0.f;
       auto moments = [&](auto recenter_tag) {
@@ -1776,7 +1786,6 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
       Sx = oct_sum(Sx); Sy = oct_sum(Sy); g2 = oct_sum(g2); g3 = oct_sum(g3); g4 = oct_sum(g4);
       g5 = oct_sum(g5); g6 = oct_sum(g6); g7 = oct_sum(g7); g8 = oct_sum(g8); g9 = oct_sum(g9);
       if (col == 0) {
-        const float q00 = ia.z, qo = ib.x, q11 = ia.w;
         // dmu = -(2 q00 Sx + qo Sy, qo Sx + 2 q11 Sy)
         const float g0 = -(2.f * q00 * Sx + qo * Sy), g1 = -(qo * Sx + 2.f * q11 * Sy);
         const size_t sq = (size_t)slot * (uint32_t)ncell + (uint32_t)qb;
@@ -1804,7 +1813,8 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
     // this word's records stay in registers (staged chunk by chunk below)
     // while the next word's are fetched into r0..r2 (staging a whole word's
     // records, 3 KB of LDS, cost occupancy: -13 us when chunked)
-    const float4 c0 = r0, c1 = r1, c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
+    // (the conic staged as -Q/2: phase A computes t = -s/2; phase B undoes it)
+    const float4 c0 = stage_conic0(r0), c1 = stage_conic1(r1), c2 = make_float4(r2.x, r2.y, __uint_as_float(slot), 0.f);
     const unsigned long long simple_w = __builtin_amdgcn_ballot_w64(mine && simple_entry(r0, r1));
     const unsigned long long mnext = wd + 1u < nwords ? live_word(wd + 1u) : 0ull;
     fetch(wd + 1u, mnext);  // in flight while this word replays
@@ -1835,19 +1845,19 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
       const uint32_t bit = (uint32_t)__builtin_ctzll(m);
       m &= m - 1ull;
       cm |= 1ull << bit;
-      // two b128 broadcasts and a b64: (mx my q00 q11) (qo o r g) (b z);
-      // pq = (q00, q11), po = (qo, opacity)
+      // two b128 broadcasts and a b64: (mx my h00 h11) (ho o r g) (b z), h = -q/2;
+      // pq = (h00, h11), po = (ho, opacity)
       const float4 r0v = reinterpret_cast<const float4 *>(cb + 48 * kk)[0];
       const float4 r1v = reinterpret_cast<const float4 *>(cb + 48 * kk)[1];
       const float2 pbz = reinterpret_cast<const float2 *>(cb + 48 * kk)[4];
       const float2 pm = make_float2(r0v.x, r0v.y), pq = make_float2(r0v.z, r0v.w);
       const float2 po = make_float2(r1v.x, r1v.y), prg = make_float2(r1v.z, r1v.w);
       const float dx = fx - pm.x, dy = fy - pm.y;
-      const float sq = conic_s(dx, dy, pq.x, po.x, pq.y);
+      const float tq = conic_s(dx, dy, pq.x, po.x, pq.y);  // -s/2, as in the forward
       // the w < 1e-5 skip on s, as in the forward (NaN falls through); `run`
       // is the forward's "A < 0.995 before this entry", carried from the
       // previous entry's own test -- the same decisions as i < n_eval
-      const bool live = run && !(sq > kSkipS);
+      const bool live = run && !(tq < kSkipT);
       uint32_t n_run = 0;
       if constexpr (kStats) n_run = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(run));
       const float X = __builtin_fmaf(gR0, prg.x, __builtin_fmaf(gR1, prg.y, __builtin_fmaf(gR2, pbz.x, gD * pbz.y)));
@@ -1858,7 +1868,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
         // u = o w in [0, 1], so both clamps are identities and pass their
         // gradients -- the general path below with its clamp tests removed,
         // the same values.  wv = 0 exactly where the pair is skipped.
-        const float w = exp_neg_half(sq);
+        const float w = exp_blend(tq);
         const float wv = live ? w : 0.f;
         const float trans = T1;
         const float c = trans * (po.y * wv);
@@ -1874,7 +1884,7 @@ __global__ __launch_bounds__(kWave) void k_blend_bwd(gs_blend_bwd_args a, BwdSta
         dop = dal * wv;
         cw = c;
       } else {
-        const float e = exp_inrange(-0.5f * sq);
+        const float e = exp_blend(tq);
         const float w = sat01(e);
         const float u = po.y * w;
         const float ai = sat01(u);
