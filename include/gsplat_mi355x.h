@@ -33,11 +33,12 @@ extern "C" {
 
 #define GS_ABI_VERSION 21
 #define GS_DEFAULT_TILE 16    /* renderer.py:24 tile_size default */
-#define GS_MAX_TILE 32768     /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
+#define GS_MAX_TILE 16384     /* tile_size in [1, GS_MAX_TILE]; the reference accepts any int, and a tile
                                  of at least max(W, H) renders the same as any larger one (one tile
                                  holds the image), so callers clamp to max(W, H): images up to
-                                 32768 px on an edge render as one tile (ceil(L/8)^2 <= 16.8 M cells,
-                                 8 x that many blend workgroups, within the grid's 2^31) */
+                                 16384 px on an edge render as one tile (ceil(L/8)^2 <= 4.2 M cells;
+                                 the blend launches one 64-lane workgroup per cell of 8 tile slots,
+                                 and a launch's work-items stay below 2^32) */
 #define GS_QUAD 8             /* pixel cells of 8x8, laid out from each tile's origin: a tile of
                                  edge L holds gs_tile_quads(L) = ceil(L/8)^2 of them (edge cells
                                  clipped to the tile); one 64-lane wave renders one cell */

@@ -21,7 +21,7 @@ LIB_NAME = "libgsplat_mi355x.so"
 LIB_PATH = os.environ.get("GS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 
 GS_DEFAULT_TILE = 16  # renderer.py:24
-GS_MAX_TILE = 32768
+GS_MAX_TILE = 16384
 GS_QUAD = 8  # 8x8 pixel cells per wave, ceil(tile/8)^2 per tile (gs_tile_quads)
 GS_RECORD_FLOATS = 12
 GS_PAIR_GRAD_FLOATS = 10

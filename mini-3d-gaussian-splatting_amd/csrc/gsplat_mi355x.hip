@@ -2521,7 +2521,7 @@ bool cam_ok(const gs_camera &c) {
   if (c.tile_size < 1 || c.tile_size > GS_MAX_TILE || c.image_width <= 0 || c.image_height <= 0) return false;
   return div_up(c.image_width, c.tile_size) <= GS_MAX_TILES_AXIS && div_up(c.image_height, c.tile_size) <= GS_MAX_TILES_AXIS;
 }
-const char *kCamMsg = "%s: tile_size must be in [1, 32768], the image non-empty with at most 4096 tiles per axis";
+const char *kCamMsg = "%s: tile_size must be in [1, 16384], the image non-empty with at most 4096 tiles per axis";
 
 // A Gaussian's rectangle is at most 2 floor(r) + 1 <= 2 floor(radius_max) + 1
 // pixels wide (renderer.py:278-293), clipped to the image: its tile width
@@ -2779,7 +2779,8 @@ gs_status gs_blend_forward(const gs_blend_fwd_args *a, gs_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool t16 = a->cam.tile_size == GS_DEFAULT_TILE;
   const long long cblocks = (long long)div_up((long long)a->tiles_x * a->tiles_y, 8) * 8LL * cells_per_tile(a->cam.tile_size);
-  if (cblocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_forward");
+  // (a launch's work-items, workgroups x 64, must stay below 2^32)
+  if (cblocks * kWave > 0xffffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_forward");
   if (a->pair_counts)
     k_blend_fwd<true, false><<<(unsigned)cblocks, kWave, 0, s>>>(*a);
   else if (t16)
@@ -2809,7 +2810,7 @@ gs_status gs_blend_backward(const gs_blend_bwd_args *a, gs_stream_t stream) {
   const int num_tiles = b.tiles_x * b.tiles_y;
   if (num_tiles <= 0) return GS_OK;
   const long long blocks = (long long)div_up(num_tiles, 8) * 8LL * b.cell_count;
-  if (blocks > 0x7fffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_backward");
+  if (blocks * kWave > 0xffffffffLL) return fail(GS_ERR_UNSUPPORTED, "%s: too many tiles", "gs_blend_backward");
   if (b.cam.tile_size == GS_DEFAULT_TILE && b.cell_count == cells)
     k_blend_bwd<true><<<(unsigned)blocks, kWave, 0, s>>>(b);
   else

@@ -62,7 +62,7 @@ def test_bad_arguments_are_reported(pkg):
     a = N.GsProjectArgs()
     a.cam.image_width = a.cam.image_height = 8
     a.key_bits = 32
-    for bad in (0, -4, 32769):  # tile_size outside [1, GS_MAX_TILE]
+    for bad in (0, -4, 16385):  # tile_size outside [1, GS_MAX_TILE]
         a.cam.tile_size = bad
         assert lib.gs_project_forward(C.byref(a), None) == 3
     with pytest.raises(RuntimeError, match="gs_status=3"):
@@ -108,8 +108,8 @@ def test_workspace_queries(pkg):
     assert lib.gs_radix_sort_workspace_bytes(4096 * 3) >= 4 * (256 * 3 + 256)
     assert lib.gs_bin_workspace_bytes(1) >= 4
     # 8x8 cells per tile: ceil(L/8)^2 (the liveness bitmap and partial layouts)
-    assert [lib.gs_tile_quads(t) for t in (1, 8, 9, 12, 16, 24, 32, 256, 0, 257, 4096, 4097, 32768, 32769)] == \
-        [1, 1, 4, 4, 4, 9, 16, 1024, 0, 1089, 262144, 263169, 4096 ** 2, 0]
+    assert [lib.gs_tile_quads(t) for t in (1, 8, 9, 12, 16, 24, 32, 256, 0, 257, 4096, 4097, 16384, 16385)] == \
+        [1, 1, 4, 4, 4, 9, 16, 1024, 0, 1089, 262144, 263169, 2048 ** 2, 0]
     # partials per entry of a one-batch backward: one per cell at every tile size (large
     # tiles may replay their cells in batches, rasterizer.cell_batch); 0 out of range
-    assert [lib.gs_partial_groups(t) for t in (1, 16, 256, 257, 4096, 0, 32769)] == [1, 4, 1024, 1089, 262144, 0, 0]
+    assert [lib.gs_partial_groups(t) for t in (1, 16, 256, 257, 4096, 0, 16385)] == [1, 4, 1024, 1089, 262144, 0, 0]

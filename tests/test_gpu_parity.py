@@ -818,7 +818,7 @@ def test_large_tiles_vs_oracle(pkg, cuda, tile):
 
 @pytest.mark.parametrize("tile", [4150, 10 ** 6])
 def test_wide_image_large_tiles_vs_oracle(pkg, cuda, tile):
-    """Tile edges above 4096 px (GS_MAX_TILE is 32768 since round 6): a
+    """Tile edges above 4096 px (GS_MAX_TILE is 16384 since round 6): a
     4200 x 40 image in two tiles of 4150 px (the second 50 px wide), and
     tile_size above the image, rendered as one tile of 4200 px -- both as the
     reference's binning (renderer.py:261-298).  519^2 / 525^2 cells per tile:
@@ -827,6 +827,18 @@ def test_wide_image_large_tiles_vs_oracle(pkg, cuda, tile):
     sc = pkg.synthetic.make_scene(2500, W, H, seed=53)
     errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.2, 0.1, 0.0), renderer_kw=dict(tile_size=tile),
                                     label=f"wide tile{tile}")
+    assert bad.sum() <= 2
+    assert not errs, errs
+
+
+def test_max_tile_edge_vs_oracle(pkg, cuda):
+    """The largest tile edge, GS_MAX_TILE = 16384: a 16384 x 8 image as one
+    tile (2048^2 cells, 33.5 M blend workgroups, the partials in dozens of
+    cell batches) against the oracle, gradients included."""
+    W, H = pkg._native.GS_MAX_TILE, 8
+    sc = pkg.synthetic.make_scene(1500, W, H, seed=59)
+    errs, bad, _ = _scene_vs_oracle(pkg, cuda, sc, W, H, (0.1, 0.2, 0.3), renderer_kw=dict(tile_size=10 ** 6),
+                                    label="max tile")
     assert bad.sum() <= 2
     assert not errs, errs
 

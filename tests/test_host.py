@@ -68,7 +68,7 @@ def test_renderer_constructor_range(pkg):
     assert pkg.camera_params(_Cam(), big, tile_size=256).groups == 1024
     # tiles above 4096 px (round 6; ABI 21 stopped at 4096): a 5000-px image as
     # one tile, or in 2 x 2 tiles of 4500 px
-    assert pkg._native.GS_MAX_TILE == 32768
+    assert pkg._native.GS_MAX_TILE == 16384
     c = pkg.camera_params(_Cam(), pkg.RenderSettings(5000, 5000, torch.zeros(3)), tile_size=10 ** 6)
     assert (c.tile_size, c.tiles_x, c.tiles_y, c.cells) == (5000, 1, 1, 625 ** 2)
     c = pkg.camera_params(_Cam(), pkg.RenderSettings(5000, 5000, torch.zeros(3)), tile_size=4500)
@@ -77,7 +77,7 @@ def test_renderer_constructor_range(pkg):
     # cover it raises, where the reference renders it as one tile
     with pytest.raises(ValueError):
         pkg.camera_params(_Cam(), pkg.RenderSettings(100, 40000, torch.zeros(3)), tile_size=10 ** 6)
-    with pytest.raises(ValueError):  # a 40000-px image in tiles above 32768 px that do not cover it
+    with pytest.raises(ValueError):  # a 70000-px image in tiles above 16384 px that do not cover it
         pkg.camera_params(_Cam(), pkg.RenderSettings(100, 70000, torch.zeros(3)), tile_size=35000)
     for bad in (dict(tile_size=0), dict(tile_size=-3), dict(tile_size=8.5), dict(radius_max=float("inf")),
                 dict(radius_min=3.0, radius_max=2.0)):
